@@ -1,0 +1,800 @@
+// fsclg.hip -- gfx950 kernels for fscl's CLR sweep scan (search_maxpos batch).
+//
+// One 512-thread workgroup (8 wave64s) owns one coarse grid cell and runs the
+// whole position bisection of scan-chromosome.c:103-139 on chip: init of the
+// start/end/mid points (init_scan_result, :58-101), and for each point the
+// alpha search of sm-search.c:269-300 as two phases (11 coarse, 14-15 refine
+// candidates).  A phase evaluates every candidate's bidirectional walk
+// (sm-search.c:105-150) as a contiguous index range found by binary search
+// (log(alpha*d) is monotone in |d|), splits the walks into 1024-term segments
+// that the 8 waves pull from an LDS counter, and sums each walk EXACTLY as the
+// reference's sequential `sm_logl += term` would, in any order:
+//
+//   inside the binade of the start value N (the window null sum) every
+//   sequential add is  S += rne(t/u)  with u = ulp(N), an integer; ties
+//   (t/u = F + 1/2) round to the even running sum, so each tie needs only the
+//   PARITY of the prefix, which is a popcount of ballots.  Per lane: int64
+//   sums of the positive / negative parts; per segment: a parity bit; per tie:
+//   its in-segment prefix parity.  A walk whose partial sums may leave the
+//   binade is "unsafe": it gets a rigorous approximation + error bound, and is
+//   re-summed sequentially only if it could be the argmax (never observed).
+//
+// Arithmetic is compiled with contraction off (no FMA fusing): the reference's
+// polynomial and log(alpha d) adds are reproduced operation for operation.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+
+#include <vector>
+
+#include "../../../include/fsclg.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int WG = 512;
+constexpr int NWAVE = WG / 64;
+constexpr int SEG = 1024;          // terms per work segment
+constexpr int MAXWALK = 32;        // 2 points x 16 candidates
+constexpr int MAXSEG_W = 192;      // segments per walk (161 at 163841 terms)
+constexpr int SEGWORDS = MAXSEG_W / 32;
+constexpr int MAXTIES = 2048;
+constexpr int MAXREF = 16;
+constexpr double LOG_AD_MIN = -20.0;  // fscl.h:79
+constexpr double LOG_AD_MAX = 4.0;    // fscl.h:80
+
+enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2 };
+
+struct Params {
+  const int32_t* pos;
+  const uint32_t* row;
+  const double* logt;
+  const double* coef;
+  const double* nullrow;
+  const int32_t* chr_start;
+  const int32_t* chr_n;
+  const double* chr_null;
+  const double* la_coarse;     // [n_coarse]
+  const double* la_refine;     // [n_coarse + 1][MAXREF]; row n_coarse: around LOG_AD_MAX
+  const int32_t* n_refine;     // [n_coarse + 1]
+  const fsclg_cell_t* cells;
+  fsclg_point_t* out;
+  unsigned long long* stats;   // 8 counters
+  int n_coarse;
+  int n_iv;
+  double step;
+  int eval_range;
+  int bp_resl;
+  int n_cells;
+  int mode;                    // 0: search_maxpos on cells, 1: search_maxalpha on given points
+};
+
+struct Pt {                     // one scan point being evaluated (scan_pt_t subset)
+  int chr, nearest, sweep, wstart, wend, n_snps, flags, pad;
+  double N, inv_u, u, la, sm, clr;
+};
+
+struct Walk {
+  int p;          // point slot
+  int nl, nr;     // terms left / right of the nearest SNP
+  int len;        // 0 (nearest already outside log(ad) <= 4) or 1 + nl + nr
+  int seg0;       // first global segment id
+  int nseg;
+  double la;
+};
+
+struct Smem {
+  Pt pt[3];
+  Walk w[MAXWALK];
+  unsigned long long P[MAXWALK];
+  unsigned long long Q[MAXWALK];
+  unsigned int segbits[MAXWALK][SEGWORDS];
+  int wflag[MAXWALK];
+  int exact[MAXWALK];
+  double val[MAXWALK];
+  double appr[MAXWALK];
+  double bnd[MAXWALK];
+  int ties[MAXTIES];
+  int n_ties;
+  int seg_next;
+  int seg_total;
+  int nwalk;
+  int need_slow[MAXWALK];
+  int n_slow;
+  int best[3];
+  unsigned long long cnt[8];
+};
+
+__device__ __forceinline__ double logt_dev(int d, const double* __restrict__ LT) {
+  // sm-search.c:40-46
+  if (d < 0) d = -d;
+  if (d > 0xFFFFFF) return 11.783502069519070 + LT[d >> 16];
+  if (d > 0xFFFF) return 5.545177444479562 + LT[d >> 8];
+  return LT[d];
+}
+
+__device__ __forceinline__ double log_ad_of(int i, int sweep, double la, const Params& P) {
+  return logt_dev(P.pos[i] - sweep, P.logt) + la;
+}
+
+// snp_likelihood (sm-search.c:85-103) with spline_interpolate (sm-spline.c:48-60)
+__device__ __forceinline__ double term_dev(int i, int sweep, double la, const Params& P) {
+  const double x = log_ad_of(i, sweep, la, P);
+  int iv = (int)((x - LOG_AD_MIN) / P.step);
+  if (iv >= P.n_iv) iv = P.n_iv - 1;
+  if (iv < 0) iv = 0;
+  const uint32_t r = P.row[i];
+  const double2* cp = reinterpret_cast<const double2*>(P.coef + ((size_t)r * (size_t)P.n_iv + (size_t)iv) * 4);
+  const double2 a = cp[0], b = cp[1];
+  const double y = x * (a.x * x * x + a.y * x + b.x) + b.y;
+  return y - P.nullrow[r];
+}
+
+__device__ __forceinline__ int walk_index(int k, int nearest, int nl) {
+  return k == 0 ? nearest : (k <= nl ? nearest - k : nearest + (k - nl));
+}
+
+__device__ __forceinline__ long long wave_sum64(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// init_scan_result (scan-chromosome.c:58-101) for one point, one thread
+__device__ void init_point(Pt& pt, int chr, int pos, const Params& P) {
+  const int a = P.chr_start[chr], n = P.chr_n[chr];
+  int i = 0, j = n;
+  while (j - i > 1) {  // search_snppos, scan-chromosome.c:39-56
+    const int m = (i + j) / 2;
+    if (P.pos[a + m] < pos) i = m; else j = m;
+  }
+  int near;
+  if (j == n) near = n - 1;
+  else if ((long long)pos - P.pos[a + i] < (long long)P.pos[a + j] - pos) near = i;
+  else near = j;
+  near += a;
+  // Q3: the de-collision loop compares a global index with the chromosome's count
+  for (int ii = near; ii < n && P.pos[ii] == pos; ii++) pos++;
+  const int cs = a, ce = a + n - 1, er = P.eval_range;
+  int ws, we;
+  if (near - er < cs) {
+    ws = cs; we = cs + er * 2; if (we > ce) we = ce;
+  } else if (near + er > ce) {
+    we = ce; ws = ce - er * 2; if (ws < cs) ws = cs;
+  } else {
+    ws = near - er; we = near + er;
+  }
+  pt.chr = chr; pt.nearest = near; pt.sweep = pos; pt.wstart = ws; pt.wend = we;
+  pt.n_snps = we - ws + 1;
+  pt.flags = 0;
+  if (ws != cs || we != ce) pt.flags |= PF_UNSUPPORTED;
+  pt.N = P.chr_null[chr];
+}
+
+// binade constants of the start value N: |N| in [2^e, 2^(e+1)), u = 2^(e-52)
+__device__ __forceinline__ void set_binade(Pt& pt) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(pt.N);
+  const int be = (int)((bits >> 52) & 0x7FF);
+  const int e = be - 1023;
+  if (be == 0 || be == 0x7FF || pt.N >= 0.0) {  // zero / subnormal / inf / non-negative: no integer path
+    pt.u = 0.0; pt.inv_u = 0.0;
+    return;
+  }
+  pt.u = __longlong_as_double((long long)(be - 52 > 0 ? be - 52 : 1) << 52);
+  pt.inv_u = __longlong_as_double((long long)(1023 + 52 - e) << 52);
+}
+
+// the walk's index range: monotone predicate log(alpha d) > 4 on each side
+__device__ void walk_bounds(Walk& W, const Pt& pt, const Params& P, int side) {
+  const int near = pt.nearest, sweep = pt.sweep;
+  const double la = W.la;
+  if (side == 0) {
+    if (log_ad_of(near, sweep, la, P) > LOG_AD_MAX) { W.len = 0; }
+    else W.len = 1;
+    // left: the ok-set is a suffix [L, near-1]
+    int a = pt.wstart - 1, b = near;
+    if (near - 1 >= pt.wstart) {
+      while (b - a > 1) {
+        const int m = a + (b - a) / 2;
+        if (log_ad_of(m, sweep, la, P) > LOG_AD_MAX) a = m; else b = m;
+      }
+    }
+    W.nl = near - b;
+  } else {
+    // right: first element may violate alone (de-collision shift), otherwise the ok-set is a prefix
+    int r = near;
+    if (near + 1 <= pt.wend && !(log_ad_of(near + 1, sweep, la, P) > LOG_AD_MAX)) {
+      int a = near + 1, b = pt.wend + 1;
+      while (b - a > 1) {
+        const int m = a + (b - a) / 2;
+        if (log_ad_of(m, sweep, la, P) > LOG_AD_MAX) b = m; else a = m;
+      }
+      r = a;
+    }
+    W.nr = r - near;
+  }
+}
+
+// exact sequential sum of one walk by one wave (slow path, settles an argmax)
+__device__ double walk_sequential(const Walk& W, const Pt& pt, const Params& P, int lane) {
+  double acc = pt.N;
+  for (int kb = 0; kb < W.len; kb += 64) {
+    const int k = kb + lane;
+    double t = 0.0;
+    if (k < W.len) t = term_dev(walk_index(k, pt.nearest, W.nl), pt.sweep, W.la, P);
+    const int lim = W.len - kb < 64 ? W.len - kb : 64;
+    for (int l = 0; l < lim; l++) acc = acc + __shfl(t, l, 64);
+  }
+  return acc;
+}
+
+// one 1024-term segment of one walk, by one wave
+__device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane) {
+  const Walk& W = S.w[w];
+  const Pt& pt = S.pt[W.p];
+  const double inv = pt.inv_u;
+  const double lim = 4611686018427387904.0 / (double)(W.len > 0 ? W.len : 1);  // 2^62 / len: no int64 overflow
+  const int k0 = s * SEG;
+  const int k1 = (k0 + SEG < W.len) ? k0 + SEG : W.len;
+  long long pp = 0, qn = 0;
+  int par = 0;
+  bool big = false;
+  for (int kb = k0; kb < k1; kb += 64) {
+    const int k = kb + lane;
+    long long M = 0;
+    bool tie = false;
+    if (k < k1) {
+      const double t = term_dev(walk_index(k, pt.nearest, W.nl), pt.sweep, W.la, P);
+      const double q = t * inv;
+      const double F = floor(q);
+      const double fr = q - F;
+      if (!(fabs(q) < lim)) big = true;
+      else {
+        tie = fr == 0.5;
+        M = (long long)F + (fr > 0.5 ? 1 : 0);
+      }
+    }
+    if (M > 0) pp += M; else qn += M;
+    const unsigned long long low = __ballot((M & 1) != 0);
+    const unsigned long long tm = __ballot(tie);
+    if (tm) {
+      if (tie) {
+        const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        const int pre = par ^ (__popcll(low & below) & 1);
+        const int idx = atomicAdd(&S.n_ties, 1);
+        if (idx < MAXTIES) S.ties[idx] = (w << 20) | ((int)(M & 1) << 19) | (pre << 18) | k;
+      }
+    }
+    par ^= __popcll(low) & 1;
+  }
+  pp = wave_sum64(pp);
+  qn = wave_sum64(qn);
+  const bool anybig = __any(big);
+  if (lane == 0) {
+    atomicAdd(&S.P[w], (unsigned long long)pp);
+    atomicAdd(&S.Q[w], (unsigned long long)qn);
+    if (par) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
+    if (anybig) atomicOr(&S.wflag[w], 1);
+  }
+}
+
+// resolve walk w's exact value (thread per walk)
+__device__ void resolve_walk(Smem& S, int w) {
+  const Walk& W = S.w[w];
+  const Pt& pt = S.pt[W.p];
+  if (W.len == 0) { S.exact[w] = 1; S.val[w] = pt.N; return; }
+  const long long P = (long long)S.P[w], Q = (long long)S.Q[w];
+  const bool overflow = S.n_ties > MAXTIES;
+  int T = 0;
+  const int nt = S.n_ties < MAXTIES ? S.n_ties : MAXTIES;
+  for (int j = 0; j < nt; j++) T += ((S.ties[j] >> 20) == w);
+  const bool big = S.wflag[w] != 0 || pt.inv_u == 0.0;
+  const long long S0 = big ? 0 : (long long)(pt.N * pt.inv_u);
+  const long long LO = -(1ll << 53), HI = -((1ll << 52) + 1);
+  const bool safe = !big && !overflow && S0 < 0 && (S0 + Q >= LO) && (S0 + P + T <= HI);
+  if (safe) {
+    int cumpar = (int)(S0 & 1), cs = 0, adjx = 0;
+    long long adjs = 0;
+    int prevk = -1;
+    for (int c = 0; c < T; c++) {  // ties of this walk in k order
+      int bestk = 0x7fffffff, bestv = 0;
+      for (int j = 0; j < nt; j++) {
+        const int v = S.ties[j];
+        const int k = v & 0x3FFFF;
+        if ((v >> 20) == w && k > prevk && k < bestk) { bestk = k; bestv = v; }
+      }
+      prevk = bestk;
+      const int s = bestk / SEG;
+      while (cs < s) { cumpar ^= (S.segbits[w][cs >> 5] >> (cs & 31)) & 1; cs++; }
+      const int pre = (bestv >> 18) & 1, fpar = (bestv >> 19) & 1;
+      const int adj = cumpar ^ pre ^ adjx ^ fpar;
+      adjx ^= adj;
+      adjs += adj;
+    }
+    S.exact[w] = 1;
+    S.val[w] = (double)(S0 + P + Q + adjs) * pt.u;
+  } else {
+    S.exact[w] = 0;
+    if (big) {
+      S.appr[w] = __longlong_as_double(0x7FF0000000000000ll);  // unknown: forces the slow path if it matters
+      S.bnd[w] = 0.0;
+    } else {
+      const double u = pt.u, len = (double)W.len;
+      const double smax = fabs(pt.N) + ((double)P - (double)Q + len) * u;
+      S.appr[w] = (double)(S0 + P + Q) * u;
+      S.bnd[w] = 2.0 * (len * u + len * 4.440892098500626e-16 * smax) + 1e-300;
+    }
+    atomicAdd(&S.cnt[4], 1ull);
+  }
+}
+
+// evaluate S.nwalk walks (already holding p, la) -> exact values in S.val
+__device__ void eval_walks(Smem& S, const Params& P) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nw = S.nwalk;
+  if (tid < 2 * nw) walk_bounds(S.w[tid >> 1], S.pt[S.w[tid >> 1].p], P, tid & 1);
+  if (tid < nw) {
+    S.P[tid] = 0; S.Q[tid] = 0; S.wflag[tid] = 0; S.need_slow[tid] = 0;
+    for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = 0;
+  }
+  if (tid == 0) { S.n_ties = 0; S.seg_next = 0; }
+  __syncthreads();
+  if (tid == 0) {
+    int seg = 0;
+    unsigned long long terms = 0;
+    for (int w = 0; w < nw; w++) {
+      Walk& W = S.w[w];
+      W.len = W.len ? 1 + W.nl + W.nr : 0;
+      W.nseg = (W.len + SEG - 1) / SEG;
+      W.seg0 = seg;
+      seg += W.nseg;
+      terms += W.len;
+    }
+    S.seg_total = seg;
+    S.cnt[0] += terms;
+    S.cnt[2] += nw;
+  }
+  __syncthreads();
+  // waves pull segments
+  for (;;) {
+    int g = 0;
+    if (lane == 0) g = atomicAdd(&S.seg_next, 1);
+    g = __shfl(g, 0, 64);
+    if (g >= S.seg_total) break;
+    int w = 0;
+    while (w < nw - 1 && g >= S.w[w].seg0 + S.w[w].nseg) w++;  // walks own consecutive segment ranges
+    run_segment(S, w, g - S.w[w].seg0, P, lane);
+  }
+  __syncthreads();
+  if (tid < nw) resolve_walk(S, tid);
+  if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;
+  __syncthreads();
+  (void)wave;
+}
+
+// sequential argmax with strict '>' (sm-search.c:279,287) over exact values,
+// starting from a prior (the -DBL_MAX / LOG_AD_MAX initial state of
+// sm-search.c:272, or the coarse winner in the refine phase).  Returns the
+// winning walk, PRIOR if nothing beats the prior, or AMBIG after marking every
+// inexact candidate that could still win for the sequential slow path.
+constexpr int PRIOR = -1, AMBIG = -2;
+__device__ int argmax_or_mark(Smem& S, int first, int count, double prior_val) {
+  int bi = PRIOR;
+  double bv = prior_val;
+  for (int c = first; c < first + count; c++)
+    if (S.exact[c] && S.val[c] > bv) { bi = c; bv = S.val[c]; }
+  int amb = 0;
+  for (int c = first; c < first + count; c++)
+    if (!S.exact[c] && !(S.appr[c] + S.bnd[c] < bv)) { S.need_slow[c] = 1; amb = 1; }
+  return amb ? AMBIG : bi;
+}
+
+// search_maxalpha for the points in slots [p0, p0+np) (sm-search.c:269-300)
+__device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < np) set_binade(S.pt[p0 + tid]);
+  // ---- coarse phase
+  if (tid < np * P.n_coarse) {
+    const int p = tid / P.n_coarse, a = tid % P.n_coarse;
+    S.w[tid].p = p0 + p;
+    S.w[tid].la = P.la_coarse[a];
+    S.w[tid].len = 0; S.w[tid].nl = S.w[tid].nr = 0;
+  }
+  if (tid == 0) { S.nwalk = np * P.n_coarse; S.cnt[3] += np; }
+  __syncthreads();
+  for (int phase = 0; phase < 2; phase++) {
+    eval_walks(S, P);
+    // argmax per point, with slow-path settling
+    for (int round = 0; round < 2; round++) {
+      if (tid == 0) {
+        S.n_slow = 0;
+        for (int p = 0; p < np; p++) {
+          const Pt& pt = S.pt[p0 + p];
+          int first, count;
+          double pv;
+          if (phase == 0) { first = p * P.n_coarse; count = P.n_coarse; pv = -1.7976931348623157e308; }
+          else { first = pt.pad >> 8; count = pt.pad & 0xFF; pv = pt.sm; }
+          const int r = argmax_or_mark(S, first, count, pv);
+          if (r == AMBIG) S.n_slow = 1;
+          S.best[p] = r;
+        }
+      }
+      __syncthreads();
+      if (S.n_slow == 0) break;
+      // settle marked walks exactly: one wave per walk
+      for (int w = wave; w < S.nwalk; w += NWAVE) {
+        if (S.need_slow[w]) {
+          const double v = walk_sequential(S.w[w], S.pt[S.w[w].p], P, lane);
+          if (lane == 0) { S.val[w] = v; S.exact[w] = 1; S.need_slow[w] = 0; atomicAdd(&S.cnt[5], 1ull); }
+        }
+      }
+      __syncthreads();
+    }
+    if (phase == 0) {
+      // record coarse winners (or the untouched initial state), lay out refine walks
+      if (tid == 0) {
+        int nw = 0;
+        for (int p = 0; p < np; p++) {
+          const int bi = S.best[p];
+          Pt& pt = S.pt[p0 + p];
+          int ci;
+          if (bi == PRIOR) { pt.la = LOG_AD_MAX; pt.sm = -1.7976931348623157e308; ci = P.n_coarse; }
+          else { pt.la = S.w[bi].la; pt.sm = S.val[bi]; ci = bi - p * P.n_coarse; }
+          const int cnt = P.n_refine[ci];
+          pt.pad = (nw << 8) | cnt;
+          for (int r = 0; r < cnt; r++, nw++) {
+            S.w[nw].p = p0 + p;
+            S.w[nw].la = P.la_refine[ci * MAXREF + r];
+            S.w[nw].len = 0; S.w[nw].nl = S.w[nw].nr = 0;
+          }
+        }
+        S.nwalk = nw;
+      }
+      __syncthreads();
+    } else {
+      if (tid == 0) {
+        for (int p = 0; p < np; p++) {
+          Pt& pt = S.pt[p0 + p];
+          const int bi = S.best[p];
+          if (bi != PRIOR) { pt.la = S.w[bi].la; pt.sm = S.val[bi]; }
+          pt.clr = 2.0 * (pt.sm - pt.N);  // sm-search.c:298
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ void write_point(fsclg_point_t& o, const Pt& pt) {
+  o.chr = pt.chr; o.nearest_snp = pt.nearest; o.sweep_pos = pt.sweep; o.n_snps = pt.n_snps;
+  o.window_start = pt.wstart; o.window_end = pt.wend; o.flags = pt.flags; o.pad = 0;
+  o.lalpha = pt.la; o.null_logl = pt.N; o.sm_logl = pt.sm; o.clr = pt.clr;
+}
+
+__global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
+  __shared__ Smem S;
+  const int tid = threadIdx.x;
+  // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous run of cells
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int per = nb / 8, x = b % 8, slot = b / 8;
+  const int cell = (nb % 8 == 0) ? x * per + slot : b;  // grids are launched as multiples of 8
+  if (cell >= P.n_cells) return;
+  if (tid < 8) S.cnt[tid] = 0;
+  if (P.mode == 1) {
+    if (tid == 0) {
+      const fsclg_point_t& in = P.out[cell];
+      Pt& pt = S.pt[0];
+      pt.chr = in.chr; pt.nearest = in.nearest_snp; pt.sweep = in.sweep_pos; pt.wstart = in.window_start;
+      pt.wend = in.window_end; pt.n_snps = in.n_snps; pt.flags = 0; pt.N = in.null_logl;
+    }
+    __syncthreads();
+    if (tid == 0) S.cnt[1] += (unsigned long long)S.pt[0].n_snps;
+    search_maxalpha_pts(S, P, 0, 1);
+    if (tid == 0) write_point(P.out[cell], S.pt[0]);
+  } else {
+    const fsclg_cell_t c = P.cells[cell];
+    if (tid < 2) init_point(S.pt[tid], c.chr, tid == 0 ? c.start_pos : c.end_pos, P);
+    __syncthreads();
+    if (tid == 0) S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps);
+    search_maxalpha_pts(S, P, 0, 2);  // start and end points share the two phases
+    int iter = 0;
+    for (;;) {
+      const int sp = S.pt[0].sweep, ep = S.pt[1].sweep;
+      if (ep - sp <= P.bp_resl) break;
+      if (++iter > 64) { if (tid == 0) S.pt[0].flags |= PF_NOCONV; break; }
+      if (tid == 0) {
+        init_point(S.pt[2], c.chr, (sp + ep) / 2, P);
+        S.cnt[1] += (unsigned long long)S.pt[2].n_snps;
+      }
+      __syncthreads();
+      search_maxalpha_pts(S, P, 2, 1);
+      if (tid == 0) {
+        // scan-chromosome.c:116: compare exactly as written
+        if ((S.pt[0].clr + S.pt[2].clr) >= (S.pt[1].clr + S.pt[2].clr)) S.pt[1] = S.pt[2];
+        else S.pt[0] = S.pt[2];
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      const Pt& r = S.pt[0].clr > S.pt[1].clr ? S.pt[0] : S.pt[1];
+      write_point(P.out[cell], r);
+      P.out[cell].flags |= S.pt[0].flags | S.pt[1].flags;
+      S.cnt[7] += 1;
+    }
+  }
+  __syncthreads();
+  if (tid < 8 && S.cnt[tid]) atomicAdd(&P.stats[tid], S.cnt[tid]);
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------- host shim
+struct fsclg_ctx {
+  int device;
+  hipStream_t stream;
+  hipEvent_t ev0, ev1;
+  // tables
+  double* d_logt = nullptr;
+  double* d_coef = nullptr;
+  double* d_null = nullptr;
+  int n_rows = 0, n_iv = 0;
+  double step = 0.0;
+  // snps
+  int32_t* d_pos = nullptr;
+  uint32_t* d_row0 = nullptr;
+  uint32_t* d_row = nullptr;
+  int n_snps = 0;
+  int32_t* d_chr_start = nullptr;
+  int32_t* d_chr_n = nullptr;
+  double* d_chr_null = nullptr;
+  int n_chr = 0;
+  std::vector<int> h_chr_n;
+  // alpha grid
+  double* d_la_coarse = nullptr;
+  double* d_la_refine = nullptr;
+  int32_t* d_n_refine = nullptr;
+  int n_coarse = 0;
+  // io
+  fsclg_cell_t* d_cells = nullptr;
+  fsclg_point_t* d_out = nullptr;
+  int cap = 0;
+  unsigned long long* d_stats = nullptr;
+  double kernel_ms = 0.0;
+  unsigned long long launches = 0;
+};
+
+static thread_local char g_err[512];
+static int set_err(int code, const char* what, hipError_t e = hipSuccess) {
+  if (e != hipSuccess) snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
+  else snprintf(g_err, sizeof g_err, "%s", what);
+  return code;
+}
+#define HIPCHK(x, what) do { hipError_t e_ = (x); if (e_ != hipSuccess) return set_err(FSCLG_E_HIP, what, e_); } while (0)
+
+template <typename T>
+static int upload(T** dst, const T* src, size_t n, hipStream_t s) {
+  if (*dst) { hipFree(*dst); *dst = nullptr; }
+  hipError_t e = hipMalloc((void**)dst, sizeof(T) * (n ? n : 1));
+  if (e != hipSuccess) return set_err(FSCLG_E_HIP, "hipMalloc", e);
+  if (n && src) {
+    e = hipMemcpyAsync(*dst, src, sizeof(T) * n, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return set_err(FSCLG_E_HIP, "hipMemcpyAsync", e);
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return set_err(FSCLG_E_HIP, "hipStreamSynchronize", e);
+  }
+  return FSCLG_OK;
+}
+
+extern "C" {
+
+const char* fsclg_last_error(void) { return g_err; }
+
+int fsclg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int fsclg_open(int device, fsclg_ctx** out) {
+  if (!out) return set_err(FSCLG_E_ARG, "null out");
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n), "hipGetDeviceCount");
+  if (device < 0 || device >= n) return set_err(FSCLG_E_ARG, "no such device");
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  fsclg_ctx* c = new fsclg_ctx();
+  c->device = device;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+  HIPCHK(hipEventCreate(&c->ev0), "hipEventCreate");
+  HIPCHK(hipEventCreate(&c->ev1), "hipEventCreate");
+  HIPCHK(hipMalloc((void**)&c->d_stats, sizeof(unsigned long long) * 8), "hipMalloc stats");
+  HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
+  *out = c;
+  return FSCLG_OK;
+}
+
+int fsclg_close(fsclg_ctx* c) {
+  if (!c) return FSCLG_OK;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  void* ptrs[] = {c->d_logt, c->d_coef, c->d_null, c->d_pos, c->d_row0, c->d_row, c->d_chr_start, c->d_chr_n,
+                  c->d_chr_null, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
+  for (void* p : ptrs) if (p) hipFree(p);
+  hipEventDestroy(c->ev0);
+  hipEventDestroy(c->ev1);
+  hipStreamDestroy(c->stream);
+  delete c;
+  return FSCLG_OK;
+}
+
+int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coef, int n_rows, int n_iv,
+                        const double* nullrow, double log_ad_step) {
+  if (!c || !log_table || !coef || !nullrow || n_rows <= 0 || n_iv <= 0) return set_err(FSCLG_E_ARG, "tables");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  int r;
+  if ((r = upload(&c->d_logt, log_table, 0x10000, c->stream))) return r;
+  if ((r = upload(&c->d_coef, coef, (size_t)n_rows * n_iv * 4, c->stream))) return r;
+  if ((r = upload(&c->d_null, nullrow, (size_t)n_rows, c->stream))) return r;
+  c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
+  return FSCLG_OK;
+}
+
+int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int n_snps,
+                      const int32_t* chr_start, const int32_t* chr_n, int n_chr) {
+  if (!c || !pos || !row || n_snps <= 0 || !chr_start || !chr_n || n_chr <= 0) return set_err(FSCLG_E_ARG, "snps");
+  for (int i = 0; i < n_chr; i++)
+    if (chr_start[i] < 0 || chr_n[i] <= 0 || chr_start[i] + chr_n[i] > n_snps) return set_err(FSCLG_E_ARG, "chr limits");
+  for (int i = 0; i < n_snps; i++)
+    if (c->n_rows && row[i] >= (uint32_t)c->n_rows) return set_err(FSCLG_E_ARG, "row index out of table");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  int r;
+  if ((r = upload(&c->d_pos, pos, (size_t)n_snps, c->stream))) return r;
+  if ((r = upload(&c->d_row0, row, (size_t)n_snps, c->stream))) return r;
+  if ((r = upload(&c->d_row, row, (size_t)n_snps, c->stream))) return r;
+  if ((r = upload(&c->d_chr_start, chr_start, (size_t)n_chr, c->stream))) return r;
+  if ((r = upload(&c->d_chr_n, chr_n, (size_t)n_chr, c->stream))) return r;
+  if ((r = upload<double>(&c->d_chr_null, nullptr, (size_t)n_chr, c->stream))) return r;
+  c->n_snps = n_snps; c->n_chr = n_chr;
+  c->h_chr_n.assign(chr_n, chr_n + n_chr);
+  return FSCLG_OK;
+}
+
+int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
+  if (!c || !c->d_row) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  if (!row) HIPCHK(hipMemcpyAsync(c->d_row, c->d_row0, sizeof(uint32_t) * c->n_snps, hipMemcpyDeviceToDevice, c->stream), "copy rows");
+  else HIPCHK(hipMemcpyAsync(c->d_row, row, sizeof(uint32_t) * c->n_snps, hipMemcpyHostToDevice, c->stream), "copy rows");
+  return FSCLG_OK;
+}
+
+int fsclg_set_chr_null(fsclg_ctx* c, const double* chr_null) {
+  if (!c || !c->d_chr_null || !chr_null) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipMemcpyAsync(c->d_chr_null, chr_null, sizeof(double) * c->n_chr, hipMemcpyHostToDevice, c->stream), "copy null");
+  return FSCLG_OK;
+}
+
+int fsclg_set_alpha_grid(fsclg_ctx* c, const double* coarse, int n_coarse, const double* refine, const int32_t* n_refine) {
+  if (!c || !coarse || !refine || !n_refine || n_coarse <= 0 || n_coarse * 2 > MAXWALK) return set_err(FSCLG_E_ARG, "alpha grid");
+  for (int i = 0; i <= n_coarse; i++)
+    if (n_refine[i] < 0 || n_refine[i] > MAXREF) return set_err(FSCLG_E_ARG, "refine count");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  int r;
+  if ((r = upload(&c->d_la_coarse, coarse, (size_t)n_coarse, c->stream))) return r;
+  if ((r = upload(&c->d_la_refine, refine, (size_t)(n_coarse + 1) * MAXREF, c->stream))) return r;
+  if ((r = upload(&c->d_n_refine, n_refine, (size_t)(n_coarse + 1), c->stream))) return r;
+  c->n_coarse = n_coarse;
+  return FSCLG_OK;
+}
+
+static int ensure_io(fsclg_ctx* c, int n) {
+  if (n <= c->cap) return FSCLG_OK;
+  if (c->d_cells) hipFree(c->d_cells);
+  if (c->d_out) hipFree(c->d_out);
+  c->d_cells = nullptr; c->d_out = nullptr;
+  int cap = n < 1024 ? 1024 : n;
+  HIPCHK(hipMalloc((void**)&c->d_cells, sizeof(fsclg_cell_t) * cap), "hipMalloc cells");
+  HIPCHK(hipMalloc((void**)&c->d_out, sizeof(fsclg_point_t) * cap), "hipMalloc out");
+  c->cap = cap;
+  return FSCLG_OK;
+}
+
+static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
+  Params P;
+  P.pos = c->d_pos; P.row = c->d_row; P.logt = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
+  P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null;
+  P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
+  P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats;
+  P.n_coarse = c->n_coarse; P.n_iv = c->n_iv; P.step = c->step;
+  P.eval_range = eval_range; P.bp_resl = bp_resl; P.n_cells = n; P.mode = mode;
+  return P;
+}
+
+static int launch(fsclg_ctx* c, const Params& P, int n) {
+  HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
+  const int grid = (n + 7) / 8 * 8;
+  hipLaunchKernelGGL(search_maxpos_kernel, dim3(grid), dim3(WG), 0, c->stream, P);
+  HIPCHK(hipGetLastError(), "launch search_maxpos_kernel");
+  HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
+  return FSCLG_OK;
+}
+
+int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, int eval_range, int bp_resl,
+                        fsclg_point_t* out) {
+  if (!c || (!cells && n_cells) || (!out && n_cells) || n_cells < 0) return set_err(FSCLG_E_ARG, "cells");
+  if (!c->d_pos || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
+  if (n_cells == 0) return FSCLG_OK;
+  // host-side shape checks before any launch
+  if (eval_range < 0 || bp_resl < 0) return set_err(FSCLG_E_ARG, "eval_range/bp_resl");
+  for (int i = 0; i < n_cells; i++) {
+    if (cells[i].chr < 0 || cells[i].chr >= c->n_chr) return set_err(FSCLG_E_ARG, "cell chromosome");
+    const long long nchr = c->h_chr_n[cells[i].chr];
+    if (nchr > 2ll * eval_range + 1)
+      return set_err(FSCLG_E_UNSUPPORTED, "chromosome larger than 2*eval_range+1 SNPs (windowed null sums)");
+    if (nchr > (long long)MAXSEG_W * SEG) return set_err(FSCLG_E_UNSUPPORTED, "window above 196608 SNPs");
+  }
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  int r;
+  if ((r = ensure_io(c, n_cells))) return r;
+  HIPCHK(hipMemcpyAsync(c->d_cells, cells, sizeof(fsclg_cell_t) * n_cells, hipMemcpyHostToDevice, c->stream), "copy cells");
+  Params P = make_params(c, n_cells, 0, eval_range, bp_resl);
+  if ((r = launch(c, P, n_cells))) return r;
+  HIPCHK(hipMemcpyAsync(out, c->d_out, sizeof(fsclg_point_t) * n_cells, hipMemcpyDeviceToHost, c->stream), "copy out");
+  HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
+  c->kernel_ms += ms;
+  c->launches++;
+  for (int i = 0; i < n_cells; i++)
+    if (out[i].flags) return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL, "device flag");
+  return FSCLG_OK;
+}
+
+int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
+  if (!c || (!pts && n_pts) || n_pts < 0) return set_err(FSCLG_E_ARG, "points");
+  if (!c->d_pos || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
+  if (n_pts == 0) return FSCLG_OK;
+  for (int i = 0; i < n_pts; i++) {
+    const fsclg_point_t& p = pts[i];
+    if (p.window_start < 0 || p.window_end >= c->n_snps || p.window_start > p.window_end ||
+        p.nearest_snp < p.window_start || p.nearest_snp > p.window_end)
+      return set_err(FSCLG_E_ARG, "point window");
+    if (p.window_end - p.window_start + 1 > MAXSEG_W * SEG) return set_err(FSCLG_E_UNSUPPORTED, "window above 196608 SNPs");
+  }
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  int r;
+  if ((r = ensure_io(c, n_pts))) return r;
+  HIPCHK(hipMemcpyAsync(c->d_out, pts, sizeof(fsclg_point_t) * n_pts, hipMemcpyHostToDevice, c->stream), "copy pts");
+  Params P = make_params(c, n_pts, 1, 0, 0);
+  if ((r = launch(c, P, n_pts))) return r;
+  HIPCHK(hipMemcpyAsync(pts, c->d_out, sizeof(fsclg_point_t) * n_pts, hipMemcpyDeviceToHost, c->stream), "copy out");
+  HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
+  c->kernel_ms += ms;
+  c->launches++;
+  return FSCLG_OK;
+}
+
+int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
+  if (!c || !st) return set_err(FSCLG_E_ARG, "stats");
+  unsigned long long h[8];
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost), "copy stats");
+  memset(st, 0, sizeof *st);
+  st->n_terms = h[0]; st->n_null = h[1]; st->n_walks = h[2]; st->n_maxalpha = h[3];
+  st->n_unsafe = h[4]; st->n_slow = h[5]; st->n_ties = h[6]; st->n_cells = h[7];
+  st->kernel_ms = c->kernel_ms; st->n_launches = c->launches;
+  return FSCLG_OK;
+}
+
+int fsclg_reset_stats(fsclg_ctx* c) {
+  if (!c) return set_err(FSCLG_E_ARG, "stats");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
+  c->kernel_ms = 0.0; c->launches = 0;
+  return FSCLG_OK;
+}
+
+}  // extern "C"

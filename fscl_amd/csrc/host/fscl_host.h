@@ -1,0 +1,51 @@
+/* fscl_host.h -- internal declarations of the host side of fscl_amd. */
+#ifndef FSCL_HOST_H
+#define FSCL_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../../include/fscl_amd.h"
+#include "../../../include/fsclg.h"
+
+void *fh_malloc(size_t n, const char *where);
+void *fh_calloc(size_t n, size_t m, const char *where);
+void *fh_realloc(void *p, size_t n, const char *where);
+double fh_now(void);
+
+/* glibc random_r TYPE_3 stream (the reference draws glibc rand(), seeded by
+   srand(0xFD821A6) at fscl.c:280); own state so ranks and speculation can
+   replay it exactly */
+typedef struct { int32_t r[31]; int f, b; } fh_rand_t;
+void fh_srand(fh_rand_t *g, unsigned seed);
+int fh_rand(fh_rand_t *g);
+
+/* log_fact table shared by lchoose (sm-spline.c:18-39) */
+double fh_log_fact(int n);
+void fh_log_fact_reserve(int n);
+
+/* spline row layout: per depth, (n+1) unfolded then (n/2+1) folded rows */
+typedef struct {
+  int n_depths;
+  int *depth_n;      /* sample size of each depth index */
+  int *row_base;     /* first row of each depth */
+  int n_rows;
+  int n_iv;          /* spline intervals (spline_pts) */
+} fh_rowmap_t;
+
+static inline uint32_t fh_row_of(const fh_rowmap_t *m, const snp_t *s) {
+  return (uint32_t)(m->row_base[s->depth_p] + (s->folded ? m->depth_n[s->depth_p] + 1 + s->obs_freq : s->obs_freq));
+}
+
+/* current global log_ad_step (sm-spline.c:16,325) */
+double fh_log_ad_step(void);
+const double *fh_log_table(void);
+
+/* the alpha grids of search_maxalpha (sm-search.c:277-295), computed with the
+   reference's own floating-point loop */
+int fh_alpha_grid(double *coarse, int max_coarse, double *refine /* [max_coarse][16] */, int32_t *n_refine);
+
+/* ms reader */
+scan_t *fh_load_ms(const char *fname, int segment_length, int folded, int sample_first, int sample_size);
+
+#endif

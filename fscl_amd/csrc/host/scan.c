@@ -1,0 +1,633 @@
+/* scan.c -- host driver of the CLR scan and block-permutation test
+ * (scan-chromosome.c, sm-search.c entry points) over the gfx950 kernels.
+ *
+ * The host keeps what is inherently serial in the reference: the cell
+ * sequence, the block permutation drawn from the glibc rand() stream, the
+ * sequential window null sums, and the pruning pass in ascending point order
+ * (each may draw rand()).  Every search_maxpos -- the 99.6 % of the
+ * reference's time -- runs on the GPU, one workgroup per cell, in lockstep
+ * trials: host permutes -> H2D rows -> GPU evaluates all active cells ->
+ * D2H CLRs -> host prunes.  With several ranks (one process per GPU) every
+ * rank replays the same host logic and evaluates a cost-balanced contiguous
+ * share of the cells; one int64 sum-allreduce per trial assembles the CLRs.
+ */
+#include <errno.h>
+#include <float.h>
+#include <math.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/time.h>
+#include <unistd.h>
+
+#include "fscl_host.h"
+
+#define CLR_NULL_DIST_SAVE 10000 /* scan-chromosome.c:227 */
+#define PERM_SEED 0xFD821A6      /* fscl.c:280 */
+
+/* fscl.c:178-179 define these; weak so the library links standalone */
+__attribute__((weak)) int n_permute = 0;
+__attribute__((weak)) char *output_fname = NULL;
+__attribute__((weak)) char *prepend_label = NULL;
+
+/* ----------------------------------------------------------------- log table */
+static double *g_log_table = NULL;
+
+void init_log_table(void) { /* sm-search.c:14-26 */
+  int i;
+  if (g_log_table) return;
+  g_log_table = fh_malloc(sizeof(double) * 0x10000, "log_table");
+  for (i = 1; i <= 0xFFFF; i++) g_log_table[i] = log(i);
+  g_log_table[0] = 0.; /* a sweep on top of a SNP counts as 1 bp away */
+}
+const double *fh_log_table(void) { init_log_table(); return g_log_table; }
+
+/* scan-chromosome.c:23-37 */
+void compute_snp_null_model(scan_t *s, double **fsp) {
+  int i;
+  for (i = 0; i < s->n_snps; i++) {
+    snp_t *p = s->snps + i;
+    const int depth = s->sample_depths[p->depth_p];
+    if (p->folded && p->obs_freq != depth - p->obs_freq)
+      p->null_logl = log(fsp[p->depth_p][p->obs_freq] + fsp[p->depth_p][depth - p->obs_freq]);
+    else
+      p->null_logl = log(fsp[p->depth_p][p->obs_freq]);
+  }
+}
+
+/* sm-search.c:269-295: the coarse grid is an accumulated for-loop, the refine
+   grid depends only on the coarse winner, so all of them are tabulated here
+   with the reference's own floating-point loops */
+int fh_alpha_grid(double *coarse, int max_coarse, double *refine, int32_t *n_refine) {
+  const double step = (LOG_AD_MAX - LOG_AD_MIN) / 10.0;
+  double la;
+  int nc = 0, c;
+  for (la = LOG_AD_MIN; la <= LOG_AD_MAX; la += step) {
+    if (nc == max_coarse) return -1;
+    coarse[nc++] = la;
+  }
+  for (c = 0; c <= nc; c++) { /* row nc: the initial state lalpha = LOG_AD_MAX (sm-search.c:272) */
+    const double best = c < nc ? coarse[c] : LOG_AD_MAX;
+    double le = best - step, re = best + step, s2;
+    int k = 0;
+    if (le < LOG_AD_MIN) le = LOG_AD_MIN;
+    if (re > LOG_AD_MAX) re = LOG_AD_MAX;
+    s2 = (re - le) / 15.;
+    for (la = le + s2; la < re; la += s2) {
+      if (k == 16) return -2;
+      refine[c * 16 + k++] = la;
+    }
+    n_refine[c] = k;
+  }
+  return nc;
+}
+
+/* ---------------------------------------------------------- device state */
+typedef struct {
+  fsclg_ctx *ctx;
+  int device;
+  const sm_ptable_t *tab_key;
+  const snp_t *snp_key;
+  int n_snps_key;
+  uint64_t key;
+  fh_rowmap_t rm;
+  uint32_t *row;  /* row of every site (unpermuted) */
+  int32_t *pos;
+  double *nullrow;
+  int32_t *chr_start, *chr_n;
+  int n_chr;
+  /* ranks */
+  int rank, world;
+  fscl_amd_exchange_fn xfn;
+  void *xctx;
+  fscl_amd_stats_t st;
+} dev_t_;
+static dev_t_ D = {NULL, -1, NULL, NULL, 0, 0, {0, NULL, NULL, 0, 0}, NULL, NULL, NULL, NULL, NULL, 0,
+                   0, 1, NULL, NULL, {0}};
+
+int fscl_amd_set_device(int device) {
+  if (D.ctx) { fsclg_close(D.ctx); D.ctx = NULL; D.tab_key = NULL; D.snp_key = NULL; }
+  D.device = device;
+  return 0;
+}
+
+int fscl_amd_set_ranks(int rank, int world, fscl_amd_exchange_fn fn, void *ctx) {
+  if (world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return -1;
+  D.rank = rank; D.world = world; D.xfn = fn; D.xctx = ctx;
+  return 0;
+}
+
+static void dev_open(void) {
+  int r, dev = D.device;
+  if (D.ctx) return;
+  if (dev < 0) {
+    const char *e = getenv("FSCL_AMD_DEVICE");
+    if (!e) e = getenv("LOCAL_RANK");
+    dev = e ? atoi(e) : 0;
+  }
+  r = fsclg_open(dev, &D.ctx);
+  if (r != FSCLG_OK)
+    logmsg(MSG_FATAL, "fscl_amd: cannot open GPU %d (%s); the scan path runs only on the GPU", dev,
+           fsclg_last_error());
+  D.device = dev;
+}
+
+static void dev_check(int r, const char *what) {
+  if (r != FSCLG_OK) logmsg(MSG_FATAL, "fscl_amd: %s failed: %s (code %d)", what, fsclg_last_error(), r);
+}
+
+static void free_rowmap(fh_rowmap_t *m) {
+  free(m->depth_n); free(m->row_base);
+  memset(m, 0, sizeof *m);
+}
+
+/* flatten the sm_ptable_t spline trees into [row][interval][4] and upload */
+static void upload_tables(const sm_ptable_t *sm, int n_depths, const int *depth_n, const snp_t *snps,
+                          const int *idx, int n_idx) {
+  fh_rowmap_t *m = &D.rm;
+  int d, r, i;
+  double *coef, *nullrow;
+  unsigned char *seen;
+  free_rowmap(m);
+  m->n_depths = n_depths;
+  m->depth_n = fh_malloc(sizeof(int) * n_depths, "rowmap");
+  m->row_base = fh_malloc(sizeof(int) * n_depths, "rowmap");
+  m->n_rows = 0;
+  for (d = 0; d < n_depths; d++) {
+    if (sm[d].sample_size != depth_n[d])
+      logmsg(MSG_FATAL, "fscl_amd: sweep-model table %d is for depth %d, data has %d", d, sm[d].sample_size,
+             depth_n[d]);
+    m->depth_n[d] = depth_n[d];
+    m->row_base[d] = m->n_rows;
+    m->n_rows += depth_n[d] + 1 + depth_n[d] / 2 + 1;
+  }
+  m->n_iv = sm[0].spline_func[0]->n;
+  coef = fh_malloc(sizeof(double) * (size_t)m->n_rows * m->n_iv * 4, "flat tables");
+  for (d = 0; d < n_depths; d++) {
+    const int n = depth_n[d];
+    for (r = 0; r <= n + n / 2 + 1; r++) {
+      const spline_t *sp = r <= n ? sm[d].spline_func[r] : sm[d].fspline_func[r - n - 1];
+      double *dst = coef + (size_t)(m->row_base[d] + r) * m->n_iv * 4;
+      if (sp->n != m->n_iv) logmsg(MSG_FATAL, "fscl_amd: splines with different knot counts");
+      for (i = 0; i < sp->n; i++) memcpy(dst + 4 * i, sp->coef[i], sizeof(double) * 4);
+    }
+  }
+  /* null_logl is a function of the row (scan-chromosome.c:23-37): take it from the sites */
+  nullrow = fh_calloc(m->n_rows, sizeof(double), "null rows");
+  seen = fh_calloc(m->n_rows, 1, "null rows");
+  for (i = 0; i < n_idx; i++) {
+    const snp_t *p = snps + (idx ? idx[i] : i);
+    const uint32_t rr = fh_row_of(m, p);
+    if (!seen[rr]) { nullrow[rr] = p->null_logl; seen[rr] = 1; }
+    else if (memcmp(&nullrow[rr], &p->null_logl, sizeof(double)) != 0)
+      logmsg(MSG_FATAL, "fscl_amd: null_logl differs between sites of the same class (call "
+                        "compute_snp_null_model first)");
+  }
+  /* log_ad_step of the tables' knot grid (sm-spline.c:325) */
+  dev_check(fsclg_upload_tables(D.ctx, fh_log_table(), coef, m->n_rows, m->n_iv, nullrow,
+                                (LOG_AD_MAX - LOG_AD_MIN) / (m->n_iv + 1.)),
+            "upload tables");
+  free(D.nullrow);
+  D.nullrow = nullrow;
+  free(coef);
+  free(seen);
+  {
+    double coarse[16], refine[17 * 16];
+    int32_t nref[17];
+    const int nc = fh_alpha_grid(coarse, 16, refine, nref);
+    if (nc <= 0) logmsg(MSG_FATAL, "fscl_amd: alpha grid");
+    dev_check(fsclg_set_alpha_grid(D.ctx, coarse, nc, refine, nref), "alpha grid");
+  }
+}
+
+static void check_site(const scan_t *s, const snp_t *p) {
+  const int n = s->sample_depths[p->depth_p];
+  if (p->obs_freq < 0 || p->obs_freq > n || (p->folded && p->obs_freq > n / 2))
+    logmsg(MSG_FATAL, "fscl_amd: site class %d out of range for depth %d (folded=%d)", p->obs_freq, n, p->folded);
+}
+
+static uint64_t fnv1a(const void *p, size_t n, uint64_t h) {
+  const unsigned char *b = p;
+  size_t i;
+  for (i = 0; i < n; i++) { h ^= b[i]; h *= 1099511628211ull; }
+  return h;
+}
+
+/* make the device hold this scan's sites and these tables; the cache key is a
+   hash of the content (a freed and re-allocated scan may reuse addresses) */
+static void prepare(scan_t *s, sm_ptable_t *sm) {
+  int i, d;
+  uint64_t key = 1469598103934665603ull;
+  init_log_table();
+  dev_open();
+  key = fnv1a(&s->n_snps, sizeof s->n_snps, key);
+  key = fnv1a(s->snps, sizeof(snp_t) * (size_t)s->n_snps, key);
+  key = fnv1a(s->sample_depths, sizeof(int) * (size_t)s->n_depths, key);
+  for (i = 0; i < s->n_chromosomes; i++) key = fnv1a(&s->chr_limits[i].start_index, 4 * sizeof(int), key);
+  for (d = 0; d < s->n_depths; d++) {
+    const int n = sm[d].sample_size;
+    key = fnv1a(&n, sizeof n, key);
+    for (i = 0; i <= n + n / 2 + 1; i++) {
+      const spline_t *sp = i <= n ? sm[d].spline_func[i] : sm[d].fspline_func[i - n - 1];
+      key = fnv1a(sp->coef[0], sizeof(double) * 4 * (size_t)sp->n, key);
+    }
+  }
+  if (D.snp_key && key == D.key) return;
+  for (i = 0; i < s->n_snps; i++) check_site(s, s->snps + i);
+  upload_tables(sm, s->n_depths, s->sample_depths, s->snps, NULL, s->n_snps);
+  free(D.row); free(D.pos); free(D.chr_start); free(D.chr_n);
+  D.row = fh_malloc(sizeof(uint32_t) * s->n_snps, "rows");
+  D.pos = fh_malloc(sizeof(int32_t) * s->n_snps, "positions");
+  for (i = 0; i < s->n_snps; i++) {
+    D.row[i] = fh_row_of(&D.rm, s->snps + i);
+    D.pos[i] = s->snps[i].pos;
+  }
+  D.n_chr = s->n_chromosomes;
+  D.chr_start = fh_malloc(sizeof(int32_t) * D.n_chr, "chr");
+  D.chr_n = fh_malloc(sizeof(int32_t) * D.n_chr, "chr");
+  for (i = 0; i < D.n_chr; i++) {
+    D.chr_start[i] = s->chr_limits[i].start_index;
+    D.chr_n[i] = s->chr_limits[i].n_snps;
+  }
+  dev_check(fsclg_upload_snps(D.ctx, D.pos, D.row, s->n_snps, D.chr_start, D.chr_n, D.n_chr), "upload snps");
+  D.tab_key = sm; D.snp_key = s->snps; D.n_snps_key = s->n_snps; D.key = key;
+}
+
+/* init_scan_result's window sum (scan-chromosome.c:92-94): sequential from 0.0
+   over the whole chromosome for the given rows */
+static void chr_null_sums(const uint32_t *row, double *out) {
+  int c, i;
+  for (c = 0; c < D.n_chr; c++) {
+    double acc = 0.;
+    for (i = D.chr_start[c]; i < D.chr_start[c] + D.chr_n[c]; i++) acc += D.nullrow[row[i]];
+    out[c] = acc;
+  }
+}
+
+/* contiguous share [lo, hi) of n items for one rank: item i belongs to the
+   rank whose slice of the total cost holds the cost accumulated before i */
+void fscl_amd_partition(const double *cost, int n, int rank, int world, int *lo, int *hi) {
+  double tot = 0., acc = 0.;
+  int i;
+  *lo = *hi = n;
+  if (world <= 1) { *lo = 0; return; }
+  for (i = 0; i < n; i++) tot += cost[i];
+  for (i = 0; i < n; i++) {
+    int owner = tot > 0 ? (int)(acc / tot * world) : (int)((long long)i * world / n);
+    if (owner >= world) owner = world - 1;
+    if (owner >= rank && *lo == n) *lo = i;
+    if (owner > rank) { *hi = i; break; }
+    acc += cost[i];
+  }
+}
+
+static void rank_share(const double *cost, int n, int *lo, int *hi) {
+  fscl_amd_partition(cost, n, D.rank, D.world, lo, hi);
+}
+
+static void exchange(long long *buf, int n) {
+  if (D.world > 1 && n > 0)
+    if (D.xfn(buf, n, D.xctx) != 0) logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
+}
+
+/* evaluate cells on this rank's share, assemble all results on every rank */
+static void eval_cells(const fsclg_cell_t *cells, int n, int eval_range, int bp_resl, fsclg_point_t *out) {
+  double *cost = NULL;
+  int lo = 0, hi = n, i, r;
+  if (D.world > 1) {
+    cost = fh_malloc(sizeof(double) * (n ? n : 1), "cost");
+    for (i = 0; i < n; i++) cost[i] = (double)D.chr_n[cells[i].chr];
+    rank_share(cost, n, &lo, &hi);
+    memset(out, 0, sizeof(fsclg_point_t) * n);
+  }
+  for (i = lo; i < hi; i += 1 << 16) {
+    const int m = hi - i < (1 << 16) ? hi - i : (1 << 16);
+    r = fsclg_search_maxpos(D.ctx, cells + i, m, eval_range, bp_resl, out + i);
+    if (r == FSCLG_E_UNSUPPORTED)
+      logmsg(MSG_FATAL, "fscl_amd: %s. Chromosomes above %d SNPs need per-window null sums, which this "
+                        "build does not evaluate on the GPU yet.", fsclg_last_error(), 2 * eval_range + 1);
+    dev_check(r, "search_maxpos");
+  }
+  D.st.gp_evals += (unsigned long long)(hi - lo);
+  if (D.world > 1) {
+    exchange((long long *)out, (int)(n * (sizeof(fsclg_point_t) / sizeof(long long))));
+    free(cost);
+  }
+}
+
+static void to_scan_pt(scan_pt_t *p, const fsclg_point_t *o) {
+  memset(p, 0, sizeof *p);
+  p->chr = o->chr; p->nearest_snp = o->nearest_snp; p->sweep_pos = o->sweep_pos; p->n_snps = o->n_snps;
+  p->window_start = o->window_start; p->window_end = o->window_end;
+  p->lalpha = o->lalpha; p->null_logl = o->null_logl; p->sm_logl = o->sm_logl; p->clr = o->clr;
+}
+
+typedef struct { scan_pt_t p; int seq; } keyed_pt_t;
+static int pt_cmp(const void *va, const void *vb) {
+  const keyed_pt_t *a = va, *b = vb;
+  if (a->p.chr != b->p.chr) return a->p.chr < b->p.chr ? -1 : 1;
+  if (a->p.sweep_pos != b->p.sweep_pos) return a->p.sweep_pos < b->p.sweep_pos ? -1 : 1;
+  return a->seq - b->seq; /* scan-chromosome.c:218-225 under glibc's stable merge sort */
+}
+
+/* scan-chromosome.c:228-265 */
+void scan_chromosome(scan_t *s, sm_ptable_t *sm, int eval_range, int bp_resl, int large_grid_sp, int n_threads) {
+  fsclg_cell_t *cells;
+  fsclg_point_t *out;
+  keyed_pt_t *kp;
+  int n = 0, cap = 1024, chm = 0, pos, i;
+  double *nul, t0 = fh_now();
+  (void)n_threads; /* the GPU evaluates every cell concurrently */
+  prepare(s, sm);
+  /* the cell sequence one scan_thread walks (scan-chromosome.c:176-212) */
+  cells = fh_malloc(sizeof(fsclg_cell_t) * cap, "cells");
+  if (s->n_chromosomes > 0) {
+    pos = s->chr_limits[0].start_pos;
+    for (;;) {
+      if (pos >= s->chr_limits[chm].bp_length) {
+        if (++chm == s->n_chromosomes) break;
+        pos = s->chr_limits[chm].start_pos;
+      }
+      if (n == cap) cells = fh_realloc(cells, sizeof(fsclg_cell_t) * (cap *= 2), "cells");
+      cells[n].chr = chm;
+      cells[n].start_pos = pos;
+      cells[n].end_pos = pos + large_grid_sp > s->chr_limits[chm].bp_length ? s->chr_limits[chm].bp_length
+                                                                             : pos + large_grid_sp;
+      cells[n].pad = 0;
+      n++;
+      pos += large_grid_sp;
+    }
+  }
+  nul = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
+  chr_null_sums(D.row, nul);
+  dev_check(fsclg_set_rows(D.ctx, NULL), "set rows");
+  dev_check(fsclg_set_chr_null(D.ctx, nul), "set null sums");
+  out = fh_malloc(sizeof(fsclg_point_t) * (n ? n : 1), "points");
+  eval_cells(cells, n, eval_range, bp_resl, out);
+  kp = fh_malloc(sizeof(keyed_pt_t) * (n ? n : 1), "points");
+  for (i = 0; i < n; i++) { to_scan_pt(&kp[i].p, out + i); kp[i].seq = i; }
+  qsort(kp, n, sizeof(keyed_pt_t), pt_cmp);
+  free(s->scan_pts);
+  s->scan_pts = fh_malloc(sizeof(scan_pt_t) * (n ? n : 1), "scan points");
+  for (i = 0; i < n; i++) s->scan_pts[i] = kp[i].p;
+  s->n_scan_pts = n;
+  free(kp); free(out); free(cells); free(nul);
+  D.st.scan_s += fh_now() - t0;
+  logmsg(MSG_STATUS, "\nInitial scan finished.\n");
+}
+
+/* ------------------------------------------------------------ permutation */
+/* scan-chromosome.c:336-389 on the row array: blocks of consecutive sites
+   (length ~ 1 + Exp(nbp), extended to at least scan_width_mb on the same
+   chromosome) are swapped into place; positions never move.  Q9: a block
+   running past the end is shifted left (j -= k - n) instead of indexing
+   p[-m] as the reference does; such events are counted. */
+static void block_permute(uint32_t *prow, const uint32_t *row, const snp_t *snps, int n, double nbp,
+                          double width_mb, fh_rand_t *g) {
+  int i = 0, j, k;
+  const double width = width_mb * 1e6;
+  memcpy(prow, row, sizeof(uint32_t) * n);
+  while (i < n) {
+    const int r1 = fh_rand(g), r2 = fh_rand(g);
+    j = r1 / (2147483647 + 1.0) * n;
+    if (r2 == 0) k = n; /* Q10: log(0) */
+    else k = j + (int)(-1.0 / nbp * log(r2 / (2147483647 + 1.0)));
+    while (k < n && snps[k].chr == snps[j].chr && snps[k].pos - snps[j].pos < width) k++;
+    if (i + (k - j) >= n) k = n;
+    if (k > n) { D.st.negj++; j -= k - n; k = n; }
+    for (; j < k && i < n && j < n; i++, j++) {
+      const uint32_t t = prow[i];
+      prow[i] = prow[j];
+      prow[j] = t;
+    }
+  }
+}
+
+static volatile sig_atomic_t g_sigint = 0;
+static struct timeval g_last_dump;
+static void on_sigint(int sig) { /* scan-chromosome.c:557-569 */
+  struct timeval now;
+  (void)sig;
+  gettimeofday(&now, NULL);
+  if ((now.tv_sec - g_last_dump.tv_sec) + (now.tv_usec - g_last_dump.tv_usec) / 1e6 < 10) {
+    static const char msg[] = "\nanother interrupt signal received, aborting permutation\n";
+    if (write(2, msg, sizeof msg - 1) < 0) {}
+    _exit(255);
+  }
+  g_sigint = 1;
+}
+
+static void output_clr_null_distribution(const char *fname, scan_t *s);
+
+/* scan-chromosome.c:582-652 (with --n-threads=1 pruning semantics) */
+void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, double alpha_factor, int n_threads,
+                  int eval_range, int bp_resl, int large_grid_sp, double scan_width_mb) {
+  fh_rand_t g;
+  uint32_t *prow;
+  int *act, n_act = s->n_scan_pts, i, k, trial = -1;
+  const int save = n_perm + 1 < CLR_NULL_DIST_SAVE ? n_perm + 1 : CLR_NULL_DIST_SAVE;
+  fsclg_cell_t *cells;
+  fsclg_point_t *out;
+  double *nul, t0 = fh_now();
+  struct sigaction sa;
+  (void)alpha_factor; (void)n_threads; /* -a is inert in the reference too (scan-chromosome.c:584) */
+  prepare(s, sm);
+  memset(&sa, 0, sizeof sa);
+  sa.sa_handler = on_sigint;
+  sigemptyset(&sa.sa_mask);
+  gettimeofday(&g_last_dump, NULL);
+  sigaction(SIGINT, &sa, NULL);
+  fh_srand(&g, PERM_SEED);
+  (void)fh_rand(&g); /* scan-chromosome.c:440: the single thread's usleep() draw */
+  prow = fh_malloc(sizeof(uint32_t) * s->n_snps, "permuted rows");
+  act = fh_malloc(sizeof(int) * (n_act ? n_act : 1), "active points");
+  cells = fh_malloc(sizeof(fsclg_cell_t) * (n_act ? n_act : 1), "cells");
+  out = fh_malloc(sizeof(fsclg_point_t) * (n_act ? n_act : 1), "points");
+  nul = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
+  for (i = 0; i < s->n_scan_pts; i++) {
+    act[i] = i;
+    if (!s->scan_pts[i].permute_clr) s->scan_pts[i].permute_clr = fh_malloc(sizeof(float) * (save > 0 ? save : 1), "permute_clr");
+  }
+  for (;;) {
+    double tp = fh_now();
+    block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, &g);
+    D.st.host_perm_s += fh_now() - tp;
+    trial++;
+    for (i = k = 0; i < n_act; i++)
+      if (!s->scan_pts[act[i]].permute_finished) act[k++] = act[i];
+    n_act = k;
+    cr_logmsg(MSG_STATUS, "Scanning snp block permutations... %7d (%d scan pts remaining)        ", trial, n_act);
+    if (n_act == 0 || trial > n_perm) break;
+    chr_null_sums(prow, nul);
+    dev_check(fsclg_set_rows(D.ctx, prow), "set rows");
+    dev_check(fsclg_set_chr_null(D.ctx, nul), "set null sums");
+    for (i = 0; i < n_act; i++) {
+      const scan_pt_t *q = s->scan_pts + act[i];
+      cells[i].chr = q->chr;
+      cells[i].start_pos = q->sweep_pos - (q->sweep_pos % large_grid_sp); /* Q5: G-aligned, unclipped */
+      cells[i].end_pos = cells[i].start_pos + large_grid_sp;
+      cells[i].pad = 0;
+    }
+    eval_cells(cells, n_act, eval_range, bp_resl, out);
+    D.st.trials++;
+    for (i = 0; i < n_act; i++) { /* scan-chromosome.c:488-502, ascending point order */
+      scan_pt_t *q = s->scan_pts + act[i];
+      const double clr = out[i].clr;
+      if (clr >= q->clr) {
+        q->permute_p++;
+        if (q->permute_p >= 20 && q->permute_p / (double)q->permute_n >= fh_rand(&g) / (2147483647 + 1.0))
+          q->permute_finished = 1; /* Q7: ratio uses the pre-increment count */
+      }
+      if (q->permute_n < save) q->permute_clr[q->permute_n] = (float)clr;
+      q->permute_n++;
+      if (clr < 0 || clr > 1000000 || isnan(clr))
+        fprintf(stderr, "%d\t%d\t%g\t%1.3e\n", q->chr, cells[i].start_pos, clr, exp(out[i].lalpha));
+    }
+    if (g_sigint && D.rank == 0) {
+      g_sigint = 0;
+      scan_output(output_fname, s, 0, n_permute, prepend_label);
+      if (output_fname) output_clr_null_distribution(output_fname, s);
+      gettimeofday(&g_last_dump, NULL);
+    }
+  }
+  cr_logmsg(MSG_STATUS, "Scanning snp block permutations... finished.\n");
+  signal(SIGINT, SIG_DFL);
+  dev_check(fsclg_set_rows(D.ctx, NULL), "set rows");
+  free(prow); free(act); free(cells); free(out); free(nul);
+  D.st.permute_s += fh_now() - t0;
+}
+
+/* sm-search.c:269-300 for one caller-initialised point (drop-in entry; the
+   scan path itself batches whole cells on the GPU) */
+void search_maxalpha(scan_pt_t *pt, snp_t *snps, sm_ptable_t *sm) {
+  const int ws = pt->window_start, we = pt->window_end, n = we - ws + 1;
+  int i, maxd = 0;
+  int *dn, *idx;
+  uint32_t *row;
+  int32_t *pos, cs, cn;
+  fsclg_point_t p;
+  init_log_table();
+  dev_open();
+  for (i = ws; i <= we; i++) if (snps[i].depth_p > maxd) maxd = snps[i].depth_p;
+  dn = fh_malloc(sizeof(int) * (maxd + 1), "depths");
+  for (i = 0; i <= maxd; i++) dn[i] = sm[i].sample_size;
+  idx = fh_malloc(sizeof(int) * n, "window");
+  for (i = 0; i < n; i++) idx[i] = ws + i;
+  upload_tables(sm, maxd + 1, dn, snps, idx, n);
+  row = fh_malloc(sizeof(uint32_t) * n, "rows");
+  pos = fh_malloc(sizeof(int32_t) * n, "positions");
+  for (i = 0; i < n; i++) { row[i] = fh_row_of(&D.rm, snps + ws + i); pos[i] = snps[ws + i].pos; }
+  cs = 0; cn = n;
+  dev_check(fsclg_upload_snps(D.ctx, pos, row, n, &cs, &cn, 1), "upload window");
+  D.tab_key = NULL; D.snp_key = NULL; /* the device no longer holds a whole scan */
+  memset(&p, 0, sizeof p);
+  p.chr = pt->chr; p.nearest_snp = pt->nearest_snp - ws; p.sweep_pos = pt->sweep_pos; p.n_snps = pt->n_snps;
+  p.window_start = 0; p.window_end = n - 1; p.null_logl = pt->null_logl;
+  dev_check(fsclg_search_points(D.ctx, &p, 1), "search_maxalpha");
+  pt->lalpha = p.lalpha; pt->sm_logl = p.sm_logl; pt->clr = p.clr;
+  free(dn); free(idx); free(row); free(pos);
+}
+
+/* ---------------------------------------------------------------- output */
+void scan_output(char *fname, scan_t *s, int maximum_only, int n_perm, char *label) {
+  FILE *f = stdout;
+  const scan_pt_t *best;
+  double max_clr;
+  char pos_str[64];
+  int i;
+  if (D.world > 1 && D.rank != 0) return; /* one writer */
+  if (fname) {
+    f = fopen(fname, "w");
+    if (!f) { fprintf(stderr, "Can't open output file \"%s\" (%s)", fname, strerror(errno)); return; }
+  }
+  if (s->n_scan_pts == 0) { if (fname) fclose(f); return; }
+  best = s->scan_pts;
+  max_clr = s->scan_pts[0].clr;
+  for (i = 1; i < s->n_scan_pts; i++)
+    if (s->scan_pts[i].clr > max_clr) { max_clr = s->scan_pts[i].clr; best = s->scan_pts + i; }
+  if (best->sweep_pos > 1000000)
+    snprintf(pos_str, sizeof pos_str, "chromosome %s %1.2f Mb", s->chr_limits[best->chr].name, best->sweep_pos / 1e6);
+  else if (best->sweep_pos > 2000)
+    snprintf(pos_str, sizeof pos_str, "chromosome %s %1.2f Kb", s->chr_limits[best->chr].name, best->sweep_pos / 1e3);
+  else
+    snprintf(pos_str, sizeof pos_str, "chromosome %s %d bp", s->chr_limits[best->chr].name, best->sweep_pos);
+  logmsg(MSG_STATUS, "\rOutput complete -- maximum CLR of %g at %s (alpha = %g)\n", max_clr, pos_str,
+         exp(best->lalpha));
+  if (maximum_only) {
+    if (label) fprintf(f, "%s\t", label);
+    fprintf(f, "%s\t%d\t%1.2f\t%1.3e\t%d\t%d\t%d\n", s->chr_limits[best->chr].name, best->sweep_pos, max_clr,
+            exp(best->lalpha), best->n_snps, s->snps[best->window_start].pos, s->snps[best->window_end].pos);
+    if (fname) fclose(f); /* the reference leaks the handle here (scan-chromosome.c:715) */
+    return;
+  }
+  for (i = 0; i < s->n_scan_pts; i++) {
+    const scan_pt_t *q = s->scan_pts + i;
+    if (label) fprintf(f, "%s\t", label);
+    if (n_perm > 0) {
+      /* Q8: an empirical ratio, no chi-square projection */
+      const double pv = q->permute_p < 2 ? 1.0 / q->permute_n : (q->permute_p - 1.0) / (double)(q->permute_n - 1.0);
+      fprintf(f, "%s\t%d\t%1.2f\t%1.3e\t%d\t%d\t%1.3f\n", s->chr_limits[q->chr].name, q->sweep_pos, q->clr,
+              exp(q->lalpha), q->permute_p, q->permute_n, -log10(pv));
+    } else {
+      fprintf(f, "%s\t%d\t%1.2f\t%1.3e\t%d\t%d\t%d\n", s->chr_limits[q->chr].name, q->sweep_pos, q->clr,
+              exp(q->lalpha), q->n_snps, s->snps[q->window_start].pos, s->snps[q->window_end].pos);
+    }
+  }
+  if (fname) fclose(f);
+}
+
+static int float_cmp(const void *a, const void *b) {
+  const float x = *(const float *)a, y = *(const float *)b;
+  return (x > y) - (x < y);
+}
+
+/* scan-chromosome.c:753-796 */
+static void output_clr_null_distribution(const char *fname, scan_t *s) {
+  char *fn = fh_malloc(strlen(fname) + 20, "fname");
+  FILE *f;
+  int i, j;
+  sprintf(fn, "%s-nulldist", fname);
+  f = fopen(fn, "w");
+  free(fn);
+  if (!f) { fprintf(stderr, "Can't open output file for CLR null distribution (%s)\n", strerror(errno)); return; }
+  fprintf(f, "chr\tpos\tCLR\talpha\tp\tn");
+  for (j = 0; j < CLR_NULL_DIST_SAVE; j++) fprintf(f, "\t%1.4f", j / (double)CLR_NULL_DIST_SAVE);
+  fprintf(f, "\n");
+  for (i = 0; i < s->n_scan_pts; i++) {
+    scan_pt_t *q = s->scan_pts + i;
+    const int np = q->permute_n < CLR_NULL_DIST_SAVE ? q->permute_n : CLR_NULL_DIST_SAVE;
+    if (q->permute_clr) qsort(q->permute_clr, np, sizeof(float), float_cmp);
+    fprintf(f, "%s\t%d\t%1.3f\t%1.3e\t%d\t%d", s->chr_limits[q->chr].name, q->sweep_pos, q->clr, exp(q->lalpha),
+            q->permute_p, q->permute_n);
+    for (j = 0; j < np && q->permute_clr; j++) fprintf(f, "\t%1.2f", (double)q->permute_clr[j]);
+    fprintf(f, "\n");
+  }
+  fclose(f);
+}
+
+/* ----------------------------------------------------------------- stats */
+void fscl_amd_get_stats(fscl_amd_stats_t *st) {
+  *st = D.st;
+  if (D.ctx) {
+    fsclg_stats_t g;
+    if (fsclg_get_stats(D.ctx, &g) == FSCLG_OK) {
+      st->kernel_ms = g.kernel_ms;
+      st->n_terms = g.n_terms; st->n_null = g.n_null; st->n_walks = g.n_walks; st->n_maxalpha = g.n_maxalpha;
+      st->n_unsafe = g.n_unsafe; st->n_slow = g.n_slow; st->n_ties = g.n_ties; st->n_launches = g.n_launches;
+    }
+  }
+}
+
+void fscl_amd_reset_stats(void) {
+  memset(&D.st, 0, sizeof D.st);
+  if (D.ctx) fsclg_reset_stats(D.ctx);
+}
+
+void fscl_amd_shutdown(void) {
+  if (D.ctx) fsclg_close(D.ctx);
+  D.ctx = NULL; D.tab_key = NULL; D.snp_key = NULL;
+  free(D.row); free(D.pos); free(D.chr_start); free(D.chr_n); free(D.nullrow);
+  D.row = NULL; D.pos = NULL; D.chr_start = NULL; D.chr_n = NULL; D.nullrow = NULL;
+  free_rowmap(&D.rm);
+}

@@ -44,8 +44,13 @@ def _neutral_counts(rng: np.random.Generator, n: int, count: int) -> np.ndarray:
 
 def generate(n_chr: int, chr_len: int, snps_per_chr: int, n: int, folded: float = 0.0,
              seed: int = 1, sweeps_per_chr: int = 0, sweep_scale: float = 20_000.0,
-             chr_names: list[str] | None = None, **_unused):
-    """Return a list of per-chromosome (name, pos, k, n_arr, folded_arr) arrays."""
+             chr_names: list[str] | None = None, missing: float = 0.0, max_missing: int = 4,
+             duplicates: float = 0.0, **_unused):
+    """Return a list of per-chromosome (name, pos, k, n_arr, folded_arr) arrays.
+
+    ``missing``: fraction of sites whose sample size is n - U{1..max_missing}
+    (several sample depths, as with missing genotypes); ``duplicates``: fraction
+    of sites moved onto the previous site's position (ties in position)."""
     rng = np.random.default_rng(seed)
     out = []
     for c in range(n_chr):
@@ -59,7 +64,16 @@ def generate(n_chr: int, chr_len: int, snps_per_chr: int, n: int, folded: float 
             hi = rng.random(snps_per_chr) < 0.15
             k = np.where(hit, np.where(hi, n - 1, 1), k)
         fold = (rng.random(snps_per_chr) < folded).astype(np.int64)
-        out.append((name, pos, k.astype(np.int64), np.full(snps_per_chr, n, dtype=np.int64), fold))
+        nn = np.full(snps_per_chr, n, dtype=np.int64)
+        if missing > 0:
+            m = rng.random(snps_per_chr) < missing
+            nn = np.where(m, n - rng.integers(1, max_missing + 1, size=snps_per_chr), nn)
+            k = np.minimum(k, nn - 1)
+        if duplicates > 0:
+            d = np.nonzero(rng.random(snps_per_chr) < duplicates)[0]
+            d = d[d > 0]
+            pos[d] = pos[d - 1]
+        out.append((name, pos, k.astype(np.int64), nn, fold))
     return out
 
 

@@ -1,0 +1,112 @@
+/*
+ * fsclg.h -- device shim C-ABI of the MI355X (gfx950) CLR scan kernels.
+ *
+ * Plain C, plain pointers and sizes, int status returns, no exceptions and no
+ * torch types cross this boundary.  One context per process per GPU.  It sits
+ * below the fscl.h-compatible host library (include/fscl_amd.h): the host C
+ * code (scan_chromosome / scan_permute) calls these; a maintainer can also
+ * bind them directly (ctypes stub in INTEGRATION.md).
+ *
+ * Reference interfaces each entry replaces (all in /root/reference):
+ *   fsclg_search_maxpos  -> search_maxpos() batch, scan-chromosome.c:126-139
+ *                           (with init_scan_result :58-101, search_maxalpha
+ *                           sm-search.c:269-300, sm_likelihood :105-150)
+ *   fsclg_search_points  -> search_maxalpha() on caller-initialised points,
+ *                           sm-search.c:269-300 (fscl.h:105)
+ *   fsclg_set_rows       -> the permuted snp array of one trial,
+ *                           scan-chromosome.c:443 (snp_block_permute output)
+ *   fsclg_upload_tables  -> sm_ptable_t spline tables (fscl.h:64-76) and
+ *                           log_table (sm-search.c:14-26)
+ *   fsclg_upload_snps    -> snp_t positions + chr_limits_t (fscl.h:7-33)
+ */
+#ifndef FSCLG_H
+#define FSCLG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  FSCLG_OK = 0,
+  FSCLG_E_ARG = -1,        /* bad argument / shape */
+  FSCLG_E_HIP = -2,        /* HIP runtime error (message in fsclg_last_error) */
+  FSCLG_E_STATE = -3,      /* tables / snps not uploaded */
+  FSCLG_E_UNSUPPORTED = -4,/* a window narrower than its chromosome (chromosome > 2*eval_range+1 SNPs) */
+  FSCLG_E_KERNEL = -5      /* device-side failure flag (e.g. position bisection did not converge) */
+};
+
+typedef struct fsclg_ctx fsclg_ctx;
+
+/* one coarse grid cell: search_maxpos(chr, start_pos, end_pos) */
+typedef struct {
+  int32_t chr, start_pos, end_pos, pad;
+} fsclg_cell_t;
+
+/* one evaluated scan point (the fields of scan_pt_t the path produces) */
+typedef struct {
+  int32_t chr, nearest_snp, sweep_pos, n_snps, window_start, window_end, flags, pad;
+  double lalpha, null_logl, sm_logl, clr;
+} fsclg_point_t;
+
+/* cumulative device counters (reset by fsclg_reset_stats) */
+typedef struct {
+  unsigned long long n_terms;      /* snp_likelihood evaluations */
+  unsigned long long n_null;       /* window null-sum elements (reference-equivalent count) */
+  unsigned long long n_walks;      /* sm_likelihood walks */
+  unsigned long long n_maxalpha;   /* search_maxalpha evaluations */
+  unsigned long long n_unsafe;     /* walks whose integer-ulp sum left its binade */
+  unsigned long long n_slow;       /* walks re-summed sequentially to settle an argmax */
+  unsigned long long n_ties;       /* round-half-even ties resolved by prefix parity */
+  unsigned long long n_cells;      /* search_maxpos evaluations */
+  double kernel_ms;                /* summed duration of the search kernels (HIP events) */
+  unsigned long long n_launches;
+} fsclg_stats_t;
+
+int fsclg_open(int device, fsclg_ctx **out);
+int fsclg_close(fsclg_ctx *c);
+const char *fsclg_last_error(void);
+int fsclg_device_count(void);
+
+/* log_table: 65536 doubles (log_table[0] = 0, log_table[i] = log(i));
+   coef: n_rows * n_iv * 4 doubles, row-major [row][interval][c0..c3];
+   nullrow: n_rows doubles (null_logl of a site with that row);
+   log_ad_step = (LOG_AD_MAX - LOG_AD_MIN) / (spline_pts + 1) */
+int fsclg_upload_tables(fsclg_ctx *c, const double *log_table, const double *coef, int n_rows, int n_iv,
+                        const double *nullrow, double log_ad_step);
+
+/* pos: n_snps int32 sorted within each chromosome; row: n_snps uint32 (spline row of each site);
+   chr_start/chr_n: first index and SNP count of each chromosome */
+int fsclg_upload_snps(fsclg_ctx *c, const int32_t *pos, const uint32_t *row, int n_snps,
+                      const int32_t *chr_start, const int32_t *chr_n, int n_chr);
+
+/* replace the per-site rows (one permutation trial); NULL restores the uploaded rows */
+int fsclg_set_rows(fsclg_ctx *c, const uint32_t *row);
+
+/* sequential window null sums (init_scan_result's sum from 0.0) for each chromosome's
+   whole-chromosome window, for the rows currently set */
+int fsclg_set_chr_null(fsclg_ctx *c, const double *chr_null);
+
+/* alpha grids: coarse (11 values of the for-loop at sm-search.c:277) and, for each
+   coarse argmax index c in [0, n_coarse), the refine values of sm-search.c:283-295
+   (max 16 each, row-major [c][16]); row n_coarse holds the refine values around
+   LOG_AD_MAX, used when no candidate beats the initial -DBL_MAX (sm-search.c:272) */
+int fsclg_set_alpha_grid(fsclg_ctx *c, const double *coarse, int n_coarse, const double *refine,
+                         const int32_t *n_refine);
+
+/* batched search_maxpos over n_cells cells; blocks until out[] is written */
+int fsclg_search_maxpos(fsclg_ctx *c, const fsclg_cell_t *cells, int n_cells, int eval_range, int bp_resl,
+                        fsclg_point_t *out);
+
+/* search_maxalpha on points whose chr/nearest_snp/sweep_pos/window/null_logl are
+   already set (init_scan_result done by the caller); fills lalpha/sm_logl/clr */
+int fsclg_search_points(fsclg_ctx *c, fsclg_point_t *pts, int n_pts);
+
+int fsclg_get_stats(fsclg_ctx *c, fsclg_stats_t *st);
+int fsclg_reset_stats(fsclg_ctx *c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

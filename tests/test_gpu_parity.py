@@ -1,0 +1,156 @@
+"""GPU parity: the HIP path (through the C-ABI) against the golden fixtures
+(reference-generated) and against the oracle, bit for bit: every scan point's
+position, window, lalpha, sm_logl, CLR, and the permutation counts (which pin
+the pruning and the rand() stream)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from util import CLI, GOLD, ROOT, assert_rows_equal, manifest, points_rows, read_dump, run_oracle
+import fscl_amd
+from fscl_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _kw(options):
+    kw = {}
+    for a in options:
+        k, _, v = a.lstrip("-").partition("=")
+        if k == "n-permute":
+            kw["n_permute"] = int(v)
+        elif k == "asc-depth":
+            kw["asc_depth"] = int(v)
+        elif k == "asc-minimum-freq":
+            kw["asc_min_freq"] = int(v)
+        elif k == "ascbias-background-only":
+            kw["ascbias_background_only"] = True
+        elif k == "include-invariant":
+            kw["include_invariant"] = True
+        elif k == "force-neutral-spectrum":
+            kw["force_neutral"] = True
+        elif k == "coarse-grid-spacing":
+            kw["large_grid_sp"] = int(v)
+        elif k == "permute-nbp":
+            kw["permute_nbp"] = float(v)
+        elif k == "sweep-width":
+            kw["scan_width_mb"] = float(v)
+        else:
+            raise ValueError(a)
+    return kw
+
+
+def test_device_present():
+    assert fscl_amd.device_count() >= 1
+
+
+@pytest.mark.parametrize("case", sorted(manifest()["cases"]))
+def test_gpu_matches_golden(built, tmp, case):
+    c = manifest()["cases"][case]
+    scan = fscl_amd.run(GOLD / c["input"], tmp / "o.txt", **_kw(c["options"]))
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(GOLD / f"{case}.dump"), case)
+    assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text()
+
+
+@pytest.mark.parametrize("case", ["g1_p25", "g2_grid50k", "g3_scan"])
+def test_cli_matches_golden(built, tmp, case):
+    c = manifest()["cases"][case]
+    r = subprocess.run([str(CLI), "-f", str(GOLD / c["input"]), "-o", str(tmp / "o.txt"), *c["options"]],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text()
+
+
+@pytest.mark.parametrize("name,gen,opts", [
+    ("c1_like", dict(n_chr=1, chr_len=20_000_000, snps_per_chr=10_000, n=50, seed=31, sweeps_per_chr=2), []),
+    ("multi_depth_asc", dict(n_chr=3, chr_len=6_000_000, snps_per_chr=6000, n=40, folded=0.3, seed=32,
+                             sweeps_per_chr=1, missing=0.25, max_missing=3, duplicates=0.005),
+     ["--asc-depth=10", "--asc-minimum-freq=2", "--n-permute=12"]),
+    ("dense", dict(n_chr=2, chr_len=400_000, snps_per_chr=8000, n=20, seed=33, duplicates=0.05),
+     ["--coarse-grid-spacing=25000", "--n-permute=6"]),
+])
+def test_gpu_matches_oracle(built, tmp, name, gen, opts):
+    snp = tmp / f"{name}.snp"
+    synth.write_snp_file(str(snp), synth.generate(**gen))
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), name)
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+    st = fscl_amd.get_stats()
+    assert st["n_terms"] > 0
+
+
+def test_ms_input_matches_oracle_on_converted_file(built, tmp):
+    ms = tmp / "x.ms"
+    synth.write_ms_file(str(ms), n_blocks=4, n_hap=20, n_seg=600, seed=41)
+    scan = fscl_amd.load_ms_input(ms, 2_000_000)
+    s = scan.contents
+    depth = s.sample_depths[0]
+    with open(tmp / "x.snp", "w") as f:  # the same sites as an SNP file
+        for i in range(s.n_snps):
+            p = s.snps[i]
+            f.write(f"{s.chr_limits[p.chr].name.decode()} {p.pos} {p.obs_freq} {depth} {p.folded}\n")
+    r = subprocess.run([str(CLI), "-m", str(ms), "--ms-segment-length=2000000", "-o", str(tmp / "g.txt"),
+                        "-G", "50000"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    run_oracle(tmp / "x.snp", tmp / "o.txt", ["--coarse-grid-spacing=50000"])
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+
+
+def test_search_maxalpha_dropin(built):
+    """search_maxalpha() on caller-initialised points equals the golden points."""
+    import ctypes as C
+    case = "g2_p30"
+    c = manifest()["cases"][case]
+    scan = fscl_amd.load_snp_input(GOLD / c["input"])
+    fsp = fscl_amd.background_fsp(scan)
+    tab = fscl_amd.compute_sweep_model_tables(scan, fsp)
+    fscl_amd.compute_snp_null_model(scan, fsp)
+    rows = read_dump(GOLD / f"{case}.dump")
+    L = fscl_amd.get_lib()
+    for row in rows[::7]:
+        pt = fscl_amd.ScanPtT()
+        pt.chr, pt.sweep_pos = row[0], row[1]
+        pt.null_logl = row[5]
+        pt.nearest_snp, pt.window_start, pt.window_end = row[6], row[7], row[8]
+        pt.n_snps = row[8] - row[7] + 1
+        pt.sm_logl, pt.lalpha = -1.7976931348623157e308, 4.0
+        L.search_maxalpha(C.byref(pt), scan.contents.snps, tab)
+        assert (pt.lalpha.hex(), pt.sm_logl.hex(), pt.clr.hex()) == (row[3].hex(), row[4].hex(), row[2].hex())
+
+
+def test_two_ranks_on_one_gpu_match_one_rank(built, tmp):
+    """Parity mode with 2 processes (gloo exchange, both on GPU 0)."""
+    c = manifest()["cases"]["g1_p25"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 1000), WORLD_SIZE="2",
+               FSCL_AMD_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, str(ROOT / "tests" / "mr_worker.py"), str(GOLD / c["input"]),
+                                       str(tmp / f"o{r}.txt"), *c["options"]], env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    for p in procs:
+        out, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err
+    assert (tmp / "o0.txt").read_text() == (GOLD / "g1_p25.out").read_text()
+    assert not (tmp / "o1.txt").exists()  # one writer
+
+
+def test_c2_scale_scan_and_short_permutation(built, tmp):
+    """BASELINE config 2 (100k SNPs, n=100, 200 Mb) at full size: the whole
+    initial scan and 3 permutation trials, bit-exact against the oracle."""
+    snp = tmp / "c2.snp"
+    synth.write_config(str(snp), "C2", seed=1)
+    opts = ["--n-permute=2"]
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
+    pts = fscl_amd.points(scan)
+    assert len(pts) == 2000
+    assert_rows_equal(points_rows(pts), read_dump(tmp / "o.dump"), "C2")
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()

@@ -1,0 +1,230 @@
+"""Host side of the product (no GPU needed): input, background spectra,
+asc-bias, spline tables, alpha grid, null model, partitioning, exports.
+Bit-exact against the reference's own compiled code (golden digests)."""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+import math
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from util import CLI, GOLD, ROOT, manifest
+import fscl_amd
+from fscl_amd import synth
+
+
+def _opts(options):
+    o = dict(asc_depth=0, asc_min=1, bg_only=0, inv=0)
+    for a in options:
+        if a.startswith("--asc-depth="):
+            o["asc_depth"] = int(a.split("=")[1])
+        elif a.startswith("--asc-minimum-freq="):
+            o["asc_min"] = int(a.split("=")[1])
+        elif a == "--ascbias-background-only":
+            o["bg_only"] = 1
+        elif a == "--include-invariant":
+            o["inv"] = 1
+    return o
+
+
+def _tables(snp, options):
+    o = _opts(options)
+    s = fscl_amd.load_snp_input(snp, o["inv"], 5)
+    fsp = fscl_amd.background_fsp(s, False, None, o["inv"])
+    tab = fscl_amd.compute_sweep_model_tables(s, fsp, o["asc_depth"], o["asc_min"], o["bg_only"], o["inv"])
+    return s, fsp, tab
+
+
+@pytest.mark.parametrize("case", sorted(manifest()["tables"]))
+def test_tables_bit_exact_vs_reference(built, case):
+    t = manifest()["tables"][case]
+    s, fsp, tab = _tables(GOLD / t["input"], t["options"])
+    assert s.contents.n_depths == len(t["depths"])
+    for d, want in enumerate(t["depths"]):
+        n = want["n"]
+        assert s.contents.sample_depths[d] == n
+        got_fsp = [fsp[d][k].hex() for k in range(n + 1)]
+        assert got_fsp == want["fsp"], f"depth {n}: background spectrum differs"
+        tb = tab[d]
+        blocks = []
+        for r in range(n + 1 + n // 2 + 1):
+            sp = tb.spline_func[r] if r <= n else tb.fspline_func[r - n - 1]
+            m = sp.contents.n
+            assert m == t["spline_pts"]
+            blocks.append(np.ctypeslib.as_array(sp.contents.coef[0], shape=(4 * m,)).tobytes())
+        for r, b in enumerate(blocks):
+            assert hashlib.sha256(b).hexdigest() == want["row_sha256"][r], f"depth {n} row {r}"
+        assert hashlib.sha256(b"".join(blocks)).hexdigest() == want["coef_sha256"]
+
+
+def test_spline_interpolate_matches_formula(built):
+    s, fsp, tab = _tables(GOLD / "g2.snp", [])
+    sp = tab[0].spline_func[3]
+    L = fscl_amd.get_lib()
+    step = 24.0 / 201.0
+    for x in np.linspace(-20, 4, 97):
+        i = min(max(int((x - (-20.0)) / step), 0), 199)
+        c = sp.contents.coef[i]
+        want = x * (c[0] * x * x + c[1] * x + c[2]) + c[3]
+        assert L.spline_interpolate(sp, float(x)).hex() == want.hex()
+
+
+def test_alpha_grid_is_the_reference_loop(built):
+    """sm-search.c:276-295 evaluated in Python (same IEEE double operations)."""
+    L = fscl_amd.get_lib()
+    coarse = (C.c_double * 16)()
+    refine = (C.c_double * (17 * 16))()
+    nref = (C.c_int32 * 17)()
+    nc = L.fh_alpha_grid(coarse, 16, refine, nref)
+    step = (4.0 - -20.0) / 10.0
+    want, la = [], -20.0
+    while la <= 4.0:
+        want.append(la)
+        la += step
+    assert nc == len(want) == 11 and [coarse[i] for i in range(nc)] == want
+    assert want[-1] == 4.0
+    for c in range(nc + 1):
+        best = want[c] if c < nc else 4.0
+        le, re_ = max(best - step, -20.0), min(best + step, 4.0)
+        s2 = (re_ - le) / 15.0
+        r, la = [], le + s2
+        while la < re_:
+            r.append(la)
+            la += s2
+        assert [refine[c * 16 + k] for k in range(nref[c])] == r
+        assert nref[c] in (14, 15)
+
+
+def test_null_model_and_input(built):
+    s, fsp, _ = _tables(GOLD / "g1.snp", [])
+    fscl_amd.compute_snp_null_model(s, fsp)
+    sc = s.contents
+    # input: sorted by (chromosome index, position), chromosomes in first-appearance order
+    rows = [ln.split() for ln in (GOLD / "g1.snp").read_text().splitlines()]
+    names = list(dict.fromkeys(r[0] for r in rows))
+    assert [sc.chr_limits[c].name.decode() for c in range(sc.n_chromosomes)] == names
+    assert sc.n_snps == len(rows)
+    prev = (-1, -1)
+    for i in range(sc.n_snps):
+        p = sc.snps[i]
+        assert (p.chr, p.pos) >= prev
+        prev = (p.chr, p.pos)
+        n = sc.sample_depths[p.depth_p]
+        if p.folded:
+            assert p.obs_freq <= n - p.obs_freq
+        f = fsp[p.depth_p]
+        want = math.log(f[p.obs_freq] + f[n - p.obs_freq]) if p.folded and p.obs_freq != n - p.obs_freq \
+            else math.log(f[p.obs_freq])
+        assert p.null_logl.hex() == want.hex()
+    for c in range(sc.n_chromosomes):
+        lim = sc.chr_limits[c]
+        assert sc.snps[lim.start_index].pos == lim.start_pos
+        assert sc.snps[lim.start_index + lim.n_snps - 1].pos == lim.bp_length
+
+
+def test_input_filters(built, tmp):
+    f = tmp / "x.snp"
+    f.write_text("# comment\nchromosome\n\nc1 100 3 10 0\nc1 50 0 10 0\nc1 60 10 10 0\nc1 70 2 4 0\n"
+                 "c2 5 8 10 1\nbad line\nc1 40 7 10 1\n")
+    s = fscl_amd.load_snp_input(f, False, 5).contents
+    got = [(s.snps[i].chr, s.snps[i].pos, s.snps[i].obs_freq, s.snps[i].folded) for i in range(s.n_snps)]
+    # invariant (0 / n) and depth < 5 dropped; folded counts become minor counts; sorted per chromosome
+    assert got == [(0, 40, 3, 1), (0, 100, 3, 0), (1, 5, 2, 1)]
+    s2 = fscl_amd.load_snp_input(f, True, 5).contents
+    assert s2.n_snps == 5
+
+
+def test_ms_reader_semantics(built, tmp):
+    ms = tmp / "x.ms"
+    synth.write_ms_file(str(ms), n_blocks=3, n_hap=12, n_seg=40, seed=5)
+    s = fscl_amd.load_ms_input(ms, 1_000_000, folded=False).contents
+    s_f = fscl_amd.load_ms_input(ms, 1_000_000, folded=True).contents
+    # Python restatement of the defined semantics
+    blocks, cur = [], None
+    lines = ms.read_text().splitlines()
+    i = 0
+    while i < len(lines):
+        if lines[i].startswith("//"):
+            seg = int(lines[i + 1].split()[1])
+            pos = [float(x) for x in lines[i + 2].split()[1:]]
+            hap = lines[i + 3:i + 3 + 12]
+            blocks.append((pos, hap))
+            i += 3 + 12
+        else:
+            i += 1
+    want = []
+    for b, (pos, hap) in enumerate(blocks):
+        for j, x in enumerate(pos):
+            d = sum(h[j] == "1" for h in hap)
+            if 0 < d < 12:
+                want.append((b, int(x * 1_000_000), d))
+    want.sort(key=lambda t: (t[0], t[1]))
+    got = [(s.snps[k].chr, s.snps[k].pos, s.snps[k].obs_freq) for k in range(s.n_snps)]
+    assert got == want
+    assert [s.chr_limits[c].name.decode() for c in range(s.n_chromosomes)] == ["1", "2", "3"]
+    assert all(s_f.snps[k].folded == 1 and s_f.snps[k].obs_freq == min(want[k][2], 12 - want[k][2])
+               for k in range(s_f.n_snps))
+
+
+def test_partition_is_contiguous_and_balanced(built):
+    rng = np.random.default_rng(0)
+    for n, world in [(10, 3), (1, 4), (0, 2), (257, 8), (40, 1)]:
+        cost = rng.integers(1, 100, size=n).astype(float)
+        spans = [fscl_amd.partition(cost, r, world) for r in range(world)]
+        covered = [i for lo, hi in spans for i in range(lo, hi)]
+        assert covered == list(range(n))
+        if n >= world * 8:
+            shares = [cost[lo:hi].sum() for lo, hi in spans]
+            assert max(shares) <= cost.sum() / world + cost.max()
+
+
+def test_library_exports_every_declared_symbol(built):
+    lib = fscl_amd.get_lib()
+    declared = set()
+    for h in (ROOT / "include").glob("*.h"):
+        txt = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        for m in re.finditer(r"^\s*(?!typedef)(?:[\w]+\s+\**)+\**(\w+)\s*\(", txt, flags=re.M):
+            if m.group(1) not in ("if", "while", "return"):
+                declared.add(m.group(1))
+    assert set(fscl_amd.EXPORTS) <= declared | {"fscl_amd_partition"}
+    for name in sorted(declared):
+        assert hasattr(lib, name), f"{name} declared in include/ but not exported"
+
+
+def test_cli_fails_loudly_without_gpu(built, tmp):
+    if fscl_amd.device_count() > 0:
+        pytest.skip("a GPU is present")
+    r = subprocess.run([str(CLI), "-f", str(GOLD / "g1.snp"), "-o", str(tmp / "o")], capture_output=True, text=True)
+    assert r.returncode != 0
+    assert "GPU" in r.stderr
+
+
+def test_cli_validation_matches_reference(built, tmp):
+    for args in (["-o", str(tmp / "o")], ["-f", str(GOLD / "g1.snp")], ["-f", "x", "-m", "y", "-o", "z"],
+                 ["-f", str(GOLD / "g1.snp"), "-o", str(tmp / "o"), "-d", "1"],
+                 ["-f", str(GOLD / "g1.snp"), "-o", str(tmp / "o"), "-g", "333"]):
+        r = subprocess.run([str(CLI), *args], capture_output=True, text=True)
+        assert r.returncode == 255, args
+
+
+def test_output_bs_and_no_scan(built, tmp):
+    bs = tmp / "bs.txt"
+    r = subprocess.run([str(CLI), "-f", str(GOLD / "g1.snp"), "-o", str(tmp / "o"), f"--output-bs={bs}", "--no-scan"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    t = manifest()["tables"]["g1"]
+    lines = bs.read_text().splitlines()
+    assert len(lines) == len(t["depths"])
+    for line, d in zip(lines, t["depths"]):
+        f = line.split("\t")
+        assert int(f[0]) == d["n"]
+        assert [float(x) for x in f[1:]] == pytest.approx([float.fromhex(h) for h in d["fsp"]], abs=5e-7)
+    # -b reads back what --output-bs wrote
+    r = subprocess.run([str(CLI), "-f", str(GOLD / "g1.snp"), "-o", str(tmp / "o"), "-b", str(bs), "--no-scan",
+                        f"--output-bs={tmp / 'bs2.txt'}"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert (tmp / "bs2.txt").read_text() == bs.read_text()
