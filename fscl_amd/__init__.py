@@ -28,7 +28,7 @@ __all__ = [
 ]
 
 ROOT = Path(__file__).resolve().parent
-LIB_PATH = ROOT / "_build" / "libfscl_amd.so"
+LIB_PATH = ROOT / ("_build_trace" if os.environ.get("FSCL_AMD_TRACE") else "_build") / "libfscl_amd.so"
 CLI_PATH = ROOT / "_build" / "fscl"
 
 

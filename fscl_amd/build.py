@@ -46,7 +46,19 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def build_native(force: bool = False) -> Path:
+def build_native(force: bool = False, trace: bool = False) -> Path:
+    """trace=True: a separate build in fscl_amd/_build_trace with device printf tracing."""
+    global OUT
+    out_saved = OUT
+    if trace:
+        OUT = PKG / "_build_trace"
+    try:
+        return _build_native(force, trace)
+    finally:
+        OUT = out_saved
+
+
+def _build_native(force: bool, trace: bool) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
     hdrs = list((ROOT / "include").glob("*.h")) + [CSRC / "host" / "fscl_host.h"]
     objs = []
@@ -59,7 +71,7 @@ def build_native(force: bool = False) -> Path:
     hip_src = CSRC / "device" / "fsclg.hip"
     hip_obj = OUT / "fsclg.o"
     if force or _stale(hip_obj, [hip_src, *hdrs]):
-        _run([ROCM / "bin" / "hipcc", *HIPFLAGS, "-c", hip_src, "-o", hip_obj])
+        _run([ROCM / "bin" / "hipcc", *HIPFLAGS, *(["-DFSCLG_TRACE"] if trace else []), "-c", hip_src, "-o", hip_obj])
     objs.append(hip_obj)
     lib = OUT / "libfscl_amd.so"
     if force or _stale(lib, objs):
@@ -84,6 +96,8 @@ def build_oracle() -> None:
 def main(argv: list[str]) -> int:
     force = "--force" in argv
     build_native(force=force)
+    if "--trace" in argv:
+        build_native(force=force, trace=True)
     if "--no-oracle" not in argv:
         build_oracle()
     return 0

@@ -32,6 +32,12 @@
 
 #pragma clang fp contract(off)
 
+#ifdef FSCLG_TRACE
+#define TRACE(...) do { if (blockIdx.x == 0 && threadIdx.x == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define TRACE(...) do {} while (0)
+#endif
+
 namespace {
 
 constexpr int WG = 512;
@@ -98,7 +104,6 @@ struct Smem {
   double bnd[MAXWALK];
   int ties[MAXTIES];
   int n_ties;
-  int seg_next;
   int seg_total;
   int nwalk;
   int need_slow[MAXWALK];
@@ -332,15 +337,16 @@ __device__ void resolve_walk(Smem& S, int w) {
 
 // evaluate S.nwalk walks (already holding p, la) -> exact values in S.val
 __device__ void eval_walks(Smem& S, const Params& P) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nw = S.nwalk;
   if (tid < 2 * nw) walk_bounds(S.w[tid >> 1], S.pt[S.w[tid >> 1].p], P, tid & 1);
   if (tid < nw) {
     S.P[tid] = 0; S.Q[tid] = 0; S.wflag[tid] = 0; S.need_slow[tid] = 0;
     for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = 0;
   }
-  if (tid == 0) { S.n_ties = 0; S.seg_next = 0; }
+  if (tid == 0) S.n_ties = 0;
   __syncthreads();
+  TRACE("  bounds done: nw=%d w0 len=%d nl=%d nr=%d\n", nw, S.w[0].len, S.w[0].nl, S.w[0].nr);
   if (tid == 0) {
     int seg = 0;
     unsigned long long terms = 0;
@@ -357,20 +363,24 @@ __device__ void eval_walks(Smem& S, const Params& P) {
     S.cnt[2] += nw;
   }
   __syncthreads();
-  // waves pull segments
-  for (;;) {
-    int g = 0;
-    if (lane == 0) g = atomicAdd(&S.seg_next, 1);
-    g = __shfl(g, 0, 64);
-    if (g >= S.seg_total) break;
+  TRACE("  layout done: segs=%d\n", S.seg_total);
+  // static round-robin of the equal-size segments over the waves; the loop
+  // counter lives in an SGPR (a per-lane atomic-dispatch loop here was
+  // miscompiled into a loop that never re-issued its atomic)
+  {
+    const int total = __builtin_amdgcn_readfirstlane(S.seg_total);
     int w = 0;
-    while (w < nw - 1 && g >= S.w[w].seg0 + S.w[w].nseg) w++;  // walks own consecutive segment ranges
-    run_segment(S, w, g - S.w[w].seg0, P, lane);
+    for (int g = wave; g < total; g += NWAVE) {
+      while (w < nw - 1 && g >= S.w[w].seg0 + S.w[w].nseg) w++;  // walks own consecutive segment ranges
+      run_segment(S, w, g - S.w[w].seg0, P, lane);
+    }
   }
   __syncthreads();
+  TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk(S, tid);
   if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;
   __syncthreads();
+  TRACE("eval_walks: nw=%d segs=%d ties=%d\n", nw, S.seg_total, S.n_ties);
   (void)wave;
 }
 
@@ -393,8 +403,9 @@ __device__ int argmax_or_mark(Smem& S, int first, int count, double prior_val) {
 
 // search_maxalpha for the points in slots [p0, p0+np) (sm-search.c:269-300)
 __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < np) set_binade(S.pt[p0 + tid]);
+  TRACE("maxalpha: p0=%d np=%d sweep=%d N=%g\n", p0, np, S.pt[p0].sweep, S.pt[p0].N);
   // ---- coarse phase
   if (tid < np * P.n_coarse) {
     const int p = tid / P.n_coarse, a = tid % P.n_coarse;
@@ -424,8 +435,9 @@ __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
       __syncthreads();
       if (S.n_slow == 0) break;
       // settle marked walks exactly: one wave per walk
-      for (int w = wave; w < S.nwalk; w += NWAVE) {
-        if (S.need_slow[w]) {
+      const int nwk = __builtin_amdgcn_readfirstlane(S.nwalk);
+      for (int w = wave; w < nwk; w += NWAVE) {
+        if (__builtin_amdgcn_readfirstlane(S.need_slow[w])) {
           const double v = walk_sequential(S.w[w], S.pt[S.w[w].p], P, lane);
           if (lane == 0) { S.val[w] = v; S.exact[w] = 1; S.need_slow[w] = 0; atomicAdd(&S.cnt[5], 1ull); }
         }

@@ -133,6 +133,13 @@ static void dev_open(void) {
   D.device = dev;
 }
 
+static int dbg(void) {
+  static int v = -1;
+  if (v < 0) v = getenv("FSCL_AMD_DEBUG") != NULL;
+  return v;
+}
+#define DBG(...) do { if (dbg()) { fprintf(stderr, "[fscl_amd] " __VA_ARGS__); fflush(stderr); } } while (0)
+
 static void dev_check(int r, const char *what) {
   if (r != FSCLG_OK) logmsg(MSG_FATAL, "fscl_amd: %s failed: %s (code %d)", what, fsclg_last_error(), r);
 }
@@ -234,6 +241,7 @@ static void prepare(scan_t *s, sm_ptable_t *sm) {
     }
   }
   if (D.snp_key && key == D.key) return;
+  DBG("prepare: uploading %d sites, %d depths\n", s->n_snps, s->n_depths);
   for (i = 0; i < s->n_snps; i++) check_site(s, s->snps + i);
   upload_tables(sm, s->n_depths, s->sample_depths, s->snps, NULL, s->n_snps);
   free(D.row); free(D.pos); free(D.chr_start); free(D.chr_n);
@@ -303,7 +311,9 @@ static void eval_cells(const fsclg_cell_t *cells, int n, int eval_range, int bp_
   }
   for (i = lo; i < hi; i += 1 << 16) {
     const int m = hi - i < (1 << 16) ? hi - i : (1 << 16);
+    DBG("search_maxpos: %d cells from %d\n", m, i);
     r = fsclg_search_maxpos(D.ctx, cells + i, m, eval_range, bp_resl, out + i);
+    DBG("search_maxpos: done (%d)\n", r);
     if (r == FSCLG_E_UNSUPPORTED)
       logmsg(MSG_FATAL, "fscl_amd: %s. Chromosomes above %d SNPs need per-window null sums, which this "
                         "build does not evaluate on the GPU yet.", fsclg_last_error(), 2 * eval_range + 1);
