@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""bench.py -- fscl CLR sweep scan + block-permutation test on MI355X.
+
+One step = one whole job of the hot path on resident inputs: the initial scan
+(search_maxpos on every grid cell) plus the permutation test (N+1 lockstep
+trials with pruning), i.e. scan_chromosome + scan_permute of the reference
+(scan-chromosome.c:228-652).  Input parsing, background spectrum, spline
+tables and the null model are set up once before the timed region.
+
+Workload (BASELINE.json configs[1], "C2"): one synthetic 200 Mb chromosome,
+100k SNPs, n = 100, 2,000 grid cells of 100 kb, 100 permutations.  With
+--gpus N (one process per GPU, torch.distributed over RCCL) the genome has N
+such chromosomes (weak scaling); ranks run the same host logic and split the
+cells, with one int64 sum-allreduce per trial (parity mode: bit-identical to
+one GPU).
+
+value = (grid points + sum of permute_n) / wall seconds over all ranks.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "grid-points × permutations / sec; max |ΔCLR| vs reference"
+UNIT = "grid-points×permutations/s"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+FP64_PEAK_TFS = 78.6       # FP64 vector
+BYTES_PER_UNIT = 8         # 8 B per SNP-term and per window-null element
+FLOPS_PER_TERM = 20        # ~20 FP64 ops per term
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--n-permute", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--workdir", default=None)
+    return ap.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    import fscl_amd
+    from fscl_amd import synth
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local)
+
+        def allreduce(arr: np.ndarray) -> None:
+            t = torch.from_numpy(arr).to(dev)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            arr[:] = t.cpu().numpy()
+
+        fscl_amd.set_ranks(rank, world, allreduce)
+    fscl_amd.set_device(local)
+
+    cfg = dict(synth.CONFIGS[args.config])
+    n_permute = cfg["n_permute"] if args.n_permute is None else args.n_permute
+    wd = Path(args.workdir or tempfile.mkdtemp(prefix="fscl_bench_"))
+    wd.mkdir(parents=True, exist_ok=True)
+    snp = wd / f"{args.config}_x{world}_r{rank}.snp"
+    gen = dict(cfg)
+    gen["n_chr"] = cfg["n_chr"] * world  # weak scaling: N x the single-GPU genome
+    synth.write_snp_file(str(snp), synth.generate(seed=args.seed, sweeps_per_chr=2, **gen))
+
+    # ---- untimed setup (input and tables reported separately)
+    t0 = time.time()
+    fscl_amd.get_lib().configure_logmsg(1)
+    fscl_amd.init_log_table()
+    scan = fscl_amd.load_snp_input(snp)
+    fsp = fscl_amd.background_fsp(scan)
+    tab = fscl_amd.compute_sweep_model_tables(scan, fsp, cfg.get("asc_depth", 0), cfg.get("asc_min_freq", 1))
+    fscl_amd.compute_snp_null_model(scan, fsp)
+    setup_s = time.time() - t0
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def job():
+        fscl_amd.scan_chromosome(scan, tab)
+        n_gp = scan.contents.n_scan_pts
+        if n_permute > 0:
+            fscl_amd.scan_permute(scan, tab, n_permute)
+        pts = fscl_amd.points(scan)
+        return n_gp, int(pts["permute_n"].sum()), pts
+
+    for _ in range(args.warmup):
+        job()
+    fscl_amd.reset_stats()
+    barrier()
+    t0 = time.perf_counter()
+    units, gp = 0, 0
+    for _ in range(args.steps):
+        n_gp, n_perm, pts = job()
+        units += n_gp + n_perm
+        gp = n_gp
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = fscl_amd.get_stats()
+
+    # ---- roofline of the dominant kernel (search_maxpos_kernel), from HIP events on its own stream
+    kernel_s = st["kernel_ms"] / 1e3
+    launches = max(1, st["n_launches"])
+    alg_bytes = BYTES_PER_UNIT * (st["n_terms"] + st["n_null"])
+    achieved = alg_bytes / kernel_s / 1e9 if kernel_s > 0 else 0.0
+    fp64 = FLOPS_PER_TERM * st["n_terms"] / kernel_s / 1e12 if kernel_s > 0 else 0.0
+
+    out = {
+        "metric": METRIC,
+        "value": units / elapsed,
+        "unit": UNIT,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded neutral-spectrum SNPs with planted sweeps, fscl_amd/synth.py)",
+        "config": {"workload": f"{args.config}: {world} x ({cfg['snps_per_chr']} SNPs, {cfg['chr_len'] // 10**6} Mb, "
+                               f"n={cfg['n']}) chromosome(s), G=100kb, {n_permute} permutations, parity mode",
+                   "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"] * world,
+                   "units_per_step": units / args.steps},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "search_maxpos_kernel", "alg_bytes_per_launch": alg_bytes / launches,
+                     "avg_launch_ms": st["kernel_ms"] / launches, "launches": st["n_launches"],
+                     "fp64_tflops": fp64, "fp64_frac": fp64 / FP64_PEAK_TFS},
+        "cpu_baseline": None,
+        "max_abs_dclr": None,
+        "setup_s": setup_s,
+        "stats": {k: st[k] for k in ("n_terms", "n_null", "n_walks", "n_unsafe", "n_slow", "n_ties", "trials",
+                                     "host_perm_s", "scan_s", "permute_s", "gp_evals")},
+    }
+
+    # ---- CPU baseline: the oracle port on the host cores, bounded sample = the initial scan
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        from oracle import OracleScan  # noqa: E402  (test infrastructure: the CPU baseline leg only)
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        orc = OracleScan(snp, threads=threads)
+        t0 = time.perf_counter()
+        orc.scan()
+        cpu_s = time.perf_counter() - t0
+        ref = orc.clr()
+        fscl_amd.scan_chromosome(scan, tab)  # the GPU's initial scan of the same genome
+        gpu = fscl_amd.points(scan)
+        assert len(ref) == len(gpu)
+        dclr = max((abs(c - g) for (_, _, c), g in zip(ref, gpu["clr"])), default=0.0)
+        mism = sum(1 for (ch, p, _), g in zip(ref, gpu) if (ch, p) != (int(g["chr"]), int(g["sweep_pos"])))
+        out["cpu_baseline"] = {"value": len(ref) / cpu_s, "unit": UNIT, "cores": threads, "kind": "port",
+                               "sample": f"initial scan of the same genome ({len(ref)} grid points), oracle/oracle.c "
+                                         f"with {threads} OpenMP threads, {cpu_s:.2f} s"}
+        out["max_abs_dclr"] = dclr
+        out["position_mismatches"] = mism
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    fscl_amd.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

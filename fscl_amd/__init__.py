@@ -28,7 +28,8 @@ __all__ = [
 ]
 
 ROOT = Path(__file__).resolve().parent
-LIB_PATH = ROOT / ("_build_trace" if os.environ.get("FSCL_AMD_TRACE") else "_build") / "libfscl_amd.so"
+LIB_PATH = (Path(os.environ["FSCL_AMD_LIBDIR"]) if os.environ.get("FSCL_AMD_LIBDIR") else
+            ROOT / ("_build_trace" if os.environ.get("FSCL_AMD_TRACE") else "_build")) / "libfscl_amd.so"
 CLI_PATH = ROOT / "_build" / "fscl"
 
 
@@ -90,7 +91,7 @@ EXPORTS = [
     "fscl_amd_get_stats", "fscl_amd_reset_stats", "fscl_amd_shutdown", "fscl_amd_partition",
     "fsclg_open", "fsclg_close", "fsclg_last_error", "fsclg_device_count", "fsclg_upload_tables",
     "fsclg_upload_snps", "fsclg_set_rows", "fsclg_set_chr_null", "fsclg_set_alpha_grid", "fsclg_search_maxpos",
-    "fsclg_search_points", "fsclg_get_stats", "fsclg_reset_stats",
+    "fsclg_search_points", "fsclg_get_stats", "fsclg_reset_stats", "fsclg_interval_thresholds",
 ]
 
 
@@ -128,6 +129,7 @@ def _load() -> C.CDLL:
         "fscl_amd_shutdown": (None, []),
         "fsclg_device_count": (C.c_int, []),
         "fsclg_last_error": (C.c_char_p, []),
+        "fsclg_interval_thresholds": (C.c_int, [C.c_double, C.c_int, P(C.c_double)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

@@ -46,19 +46,23 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def build_native(force: bool = False, trace: bool = False) -> Path:
-    """trace=True: a separate build in fscl_amd/_build_trace with device printf tracing."""
+def build_native(force: bool = False, trace: bool = False, variant: str | None = None,
+                 defines: tuple[str, ...] = ()) -> Path:
+    """trace=True: a separate build in fscl_amd/_build_trace with device printf tracing;
+    variant/defines: an experiment build in fscl_amd/_build_<variant> with extra -D flags."""
     global OUT
     out_saved = OUT
     if trace:
         OUT = PKG / "_build_trace"
+    elif variant:
+        OUT = PKG / f"_build_{variant}"
     try:
-        return _build_native(force, trace)
+        return _build_native(force, trace, defines)
     finally:
         OUT = out_saved
 
 
-def _build_native(force: bool, trace: bool) -> Path:
+def _build_native(force: bool, trace: bool, defines: tuple[str, ...] = ()) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
     hdrs = list((ROOT / "include").glob("*.h")) + [CSRC / "host" / "fscl_host.h"]
     objs = []
@@ -71,7 +75,7 @@ def _build_native(force: bool, trace: bool) -> Path:
     hip_src = CSRC / "device" / "fsclg.hip"
     hip_obj = OUT / "fsclg.o"
     if force or _stale(hip_obj, [hip_src, *hdrs]):
-        _run([ROCM / "bin" / "hipcc", *HIPFLAGS, *(["-DFSCLG_TRACE"] if trace else []), "-c", hip_src, "-o", hip_obj])
+        _run([ROCM / "bin" / "hipcc", *HIPFLAGS, *(["-DFSCLG_TRACE"] if trace else []), *defines, "-c", hip_src, "-o", hip_obj])
     objs.append(hip_obj)
     lib = OUT / "libfscl_amd.so"
     if force or _stale(lib, objs):

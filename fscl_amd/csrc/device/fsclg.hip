@@ -48,6 +48,12 @@ constexpr int MAXSEG_W = 192;      // segments per walk (161 at 163841 terms)
 constexpr int SEGWORDS = MAXSEG_W / 32;
 constexpr int MAXTIES = 2048;
 constexpr int MAXREF = 16;
+constexpr int MAXIV = 1024;        // spline intervals whose thresholds live in LDS
+constexpr int MAXROWS = 2048;      // spline rows whose null_logl lives in LDS
+#ifndef FSCLG_U
+#define FSCLG_U 4
+#endif
+constexpr int U = FSCLG_U;         // terms per lane per loop trip (independent load chains)
 constexpr double LOG_AD_MIN = -20.0;  // fscl.h:79
 constexpr double LOG_AD_MAX = 4.0;    // fscl.h:80
 
@@ -59,6 +65,7 @@ struct Params {
   const double* logt;
   const double* coef;
   const double* nullrow;
+  const double* thr;           // thr[j] = least x with (int)((x - LOG_AD_MIN) / step) >= j, j = 1..n_iv-1
   const int32_t* chr_start;
   const int32_t* chr_n;
   const double* chr_null;
@@ -70,7 +77,9 @@ struct Params {
   unsigned long long* stats;   // 8 counters
   int n_coarse;
   int n_iv;
+  int n_rows;
   double step;
+  double inv_step;
   int eval_range;
   int bp_resl;
   int n_cells;
@@ -110,31 +119,58 @@ struct Smem {
   int n_slow;
   int best[3];
   unsigned long long cnt[8];
+  double thr[MAXIV + 1];
+  double nul[MAXROWS];
 };
 
 __device__ __forceinline__ double logt_dev(int d, const double* __restrict__ LT) {
-  // sm-search.c:40-46
-  if (d < 0) d = -d;
-  if (d > 0xFFFFFF) return 11.783502069519070 + LT[d >> 16];
-  if (d > 0xFFFF) return 5.545177444479562 + LT[d >> 8];
-  return LT[d];
+  // sm-search.c:40-46, branch-free: one gather, then the same add (0.0 + x == x for x >= 0)
+  const int ad = d < 0 ? -d : d;
+  const bool b1 = ad > 0xFFFF, b2 = ad > 0xFFFFFF;
+  const int ix = b2 ? (ad >> 16) : (b1 ? (ad >> 8) : ad);
+  const double c = b2 ? 11.783502069519070 : (b1 ? 5.545177444479562 : 0.0);
+  return c + LT[ix];
 }
 
 __device__ __forceinline__ double log_ad_of(int i, int sweep, double la, const Params& P) {
   return logt_dev(P.pos[i] - sweep, P.logt) + la;
 }
 
+// spline interval of sm-spline.c:52-54, (int)((x - LOG_AD_MIN) / step) clamped, without the
+// division: a multiply estimate is within one of it, and exact thresholds settle it
+// (thr[0] = -inf and thr[n_iv] = +inf make the correction branch-free)
+template <bool LDS>
+__device__ __forceinline__ int interval_of(double x, const Smem& S, const Params& P) {
+  int iv = (int)((x - LOG_AD_MIN) * P.inv_step);
+  iv = iv < 0 ? 0 : (iv >= P.n_iv ? P.n_iv - 1 : iv);
+  double lo, hi;
+  if constexpr (LDS) { lo = S.thr[iv]; hi = S.thr[iv + 1]; }
+  else { lo = P.thr[iv]; hi = P.thr[iv + 1]; }
+  return iv + (x >= hi ? 1 : 0) - (x < lo ? 1 : 0);
+}
+
+template <bool LDS>
+__device__ __forceinline__ double null_of(uint32_t r, const Smem& S, const Params& P) {
+  if constexpr (LDS) return S.nul[r];
+  else return P.nullrow[r];
+}
+
+// coefficient block of (row, interval): interval-major [iv][row][4], so the lanes of a
+// wave (neighbouring sites, nearly equal log distance) read from one interval's rows
+__device__ __forceinline__ const double2* coef_of(uint32_t r, int iv, const Params& P) {
+  return reinterpret_cast<const double2*>(P.coef + ((size_t)(uint32_t)iv * (uint32_t)P.n_rows + r) * 4);
+}
+
 // snp_likelihood (sm-search.c:85-103) with spline_interpolate (sm-spline.c:48-60)
-__device__ __forceinline__ double term_dev(int i, int sweep, double la, const Params& P) {
+template <bool LDS>
+__device__ __forceinline__ double term_dev(int i, int sweep, double la, const Smem& S, const Params& P) {
   const double x = log_ad_of(i, sweep, la, P);
-  int iv = (int)((x - LOG_AD_MIN) / P.step);
-  if (iv >= P.n_iv) iv = P.n_iv - 1;
-  if (iv < 0) iv = 0;
+  const int iv = interval_of<LDS>(x, S, P);
   const uint32_t r = P.row[i];
-  const double2* cp = reinterpret_cast<const double2*>(P.coef + ((size_t)r * (size_t)P.n_iv + (size_t)iv) * 4);
+  const double2* cp = coef_of(r, iv, P);
   const double2 a = cp[0], b = cp[1];
   const double y = x * (a.x * x * x + a.y * x + b.x) + b.y;
-  return y - P.nullrow[r];
+  return y - null_of<LDS>(r, S, P);
 }
 
 __device__ __forceinline__ int walk_index(int k, int nearest, int nl) {
@@ -223,63 +259,108 @@ __device__ void walk_bounds(Walk& W, const Pt& pt, const Params& P, int side) {
 }
 
 // exact sequential sum of one walk by one wave (slow path, settles an argmax)
-__device__ double walk_sequential(const Walk& W, const Pt& pt, const Params& P, int lane) {
+template <bool LDS>
+__device__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, const Params& P, int lane) {
   double acc = pt.N;
   for (int kb = 0; kb < W.len; kb += 64) {
     const int k = kb + lane;
     double t = 0.0;
-    if (k < W.len) t = term_dev(walk_index(k, pt.nearest, W.nl), pt.sweep, W.la, P);
+    if (k < W.len) t = term_dev<LDS>(walk_index(k, pt.nearest, W.nl), pt.sweep, W.la, S, P);
     const int lim = W.len - kb < 64 ? W.len - kb : 64;
     for (int l = 0; l < lim; l++) acc = acc + __shfl(t, l, 64);
   }
   return acc;
 }
 
-// one 1024-term segment of one walk, by one wave
+// one 1024-term segment of one walk, by one wave: U terms per lane per trip, the
+// loads of all U issued before any is consumed, no divergent branches except
+// the (rare) tie record.  Per lane: exact int64 sum of M = rne(t/u) and of its
+// negative part (the positive part is their difference).
+template <bool LDS>
 __device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane) {
-  const Walk& W = S.w[w];
-  const Pt& pt = S.pt[W.p];
-  const double inv = pt.inv_u;
-  const double lim = 4611686018427387904.0 / (double)(W.len > 0 ? W.len : 1);  // 2^62 / len: no int64 overflow
+#ifdef FSCLG_EXP_NOTERMS  // timing ablation only: skip every term
+  return;
+#endif
+  const int near = S.pt[S.w[w].p].nearest, sweep = S.pt[S.w[w].p].sweep, nl = S.w[w].nl, len = S.w[w].len;
+  const double la = S.w[w].la, inv = S.pt[S.w[w].p].inv_u;
+  const double lim = fmin(4611686018427387904.0 / (double)(len > 0 ? len : 1), 1125899906842624.0);  // 2^62/len, 2^50
+  const double MAGIC = 6755399441055744.0;  // 1.5 * 2^52: integer-valued |v| < 2^51 -> int64 by a bit subtraction
+  const long long MAGIC_BITS = 0x4338000000000000ll;
   const int k0 = s * SEG;
-  const int k1 = (k0 + SEG < W.len) ? k0 + SEG : W.len;
-  long long pp = 0, qn = 0;
+  const int k1 = (k0 + SEG < len) ? k0 + SEG : len;
+  long long sum = 0, neg = 0;
   int par = 0;
   bool big = false;
-  for (int kb = k0; kb < k1; kb += 64) {
-    const int k = kb + lane;
-    long long M = 0;
-    bool tie = false;
-    if (k < k1) {
-      const double t = term_dev(walk_index(k, pt.nearest, W.nl), pt.sweep, W.la, P);
+  for (int kb = k0; kb < k1; kb += 64 * U) {
+    int idx[U];
+    bool act[U];
+    int pv[U];
+    uint32_t rv[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int k = kb + 64 * u + lane;
+      act[u] = k < k1;
+      const int kk = act[u] ? k : 0;
+      idx[u] = kk <= nl ? near - kk : near + (kk - nl);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) { pv[u] = P.pos[idx[u]]; rv[u] = P.row[idx[u]]; }
+    double x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#ifdef FSCLG_EXP_NOLT   // timing ablation only: no log-table gather
+      x[u] = (double)((pv[u] - sweep) & 15) + la;
+#else
+      x[u] = logt_dev(pv[u] - sweep, P.logt) + la;
+#endif
+    }
+    double2 ca[U], cb[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int iv = interval_of<LDS>(x[u], S, P);
+#ifdef FSCLG_EXP_NOCOEF  // timing ablation only: every lane reads one coefficient block
+      const double2* cp = reinterpret_cast<const double2*>(P.coef + (size_t)(iv & 1) * 4);
+#else
+      const double2* cp = coef_of(rv[u], iv, P);
+#endif
+      ca[u] = cp[0];
+      cb[u] = cp[1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
+      const double t = y - null_of<LDS>(rv[u], S, P);
       const double q = t * inv;
       const double F = floor(q);
       const double fr = q - F;
-      if (!(fabs(q) < lim)) big = true;
-      else {
-        tie = fr == 0.5;
-        M = (long long)F + (fr > 0.5 ? 1 : 0);
+      const bool ok = fabs(q) < lim;
+      big |= act[u] & !ok;
+      const bool use = act[u] & ok;
+      const bool tie = use & (fr == 0.5);
+      const double Md = F + (fr > 0.5 ? 1.0 : 0.0);
+      const long long Mv = __double_as_longlong(Md + MAGIC) - MAGIC_BITS;
+      const long long M = use ? Mv : 0;
+      sum += M;
+      neg += M < 0 ? M : 0;
+      const unsigned long long low = __ballot((M & 1) != 0);
+      const unsigned long long tm = __ballot(tie);
+      if (tm) {
+        if (tie) {
+          const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+          const int pre = par ^ (__popcll(low & below) & 1);
+          const int ti = atomicAdd(&S.n_ties, 1);
+          if (ti < MAXTIES) S.ties[ti] = (w << 20) | ((int)(M & 1) << 19) | (pre << 18) | (kb + 64 * u + lane);
+        }
       }
+      par ^= __popcll(low) & 1;
     }
-    if (M > 0) pp += M; else qn += M;
-    const unsigned long long low = __ballot((M & 1) != 0);
-    const unsigned long long tm = __ballot(tie);
-    if (tm) {
-      if (tie) {
-        const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-        const int pre = par ^ (__popcll(low & below) & 1);
-        const int idx = atomicAdd(&S.n_ties, 1);
-        if (idx < MAXTIES) S.ties[idx] = (w << 20) | ((int)(M & 1) << 19) | (pre << 18) | k;
-      }
-    }
-    par ^= __popcll(low) & 1;
   }
-  pp = wave_sum64(pp);
-  qn = wave_sum64(qn);
+  sum = wave_sum64(sum);
+  neg = wave_sum64(neg);
   const bool anybig = __any(big);
   if (lane == 0) {
-    atomicAdd(&S.P[w], (unsigned long long)pp);
-    atomicAdd(&S.Q[w], (unsigned long long)qn);
+    atomicAdd(&S.P[w], (unsigned long long)(sum - neg));
+    atomicAdd(&S.Q[w], (unsigned long long)neg);
     if (par) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
     if (anybig) atomicOr(&S.wflag[w], 1);
   }
@@ -336,6 +417,7 @@ __device__ void resolve_walk(Smem& S, int w) {
 }
 
 // evaluate S.nwalk walks (already holding p, la) -> exact values in S.val
+template <bool LDS>
 __device__ void eval_walks(Smem& S, const Params& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nw = S.nwalk;
@@ -372,7 +454,7 @@ __device__ void eval_walks(Smem& S, const Params& P) {
     int w = 0;
     for (int g = wave; g < total; g += NWAVE) {
       while (w < nw - 1 && g >= S.w[w].seg0 + S.w[w].nseg) w++;  // walks own consecutive segment ranges
-      run_segment(S, w, g - S.w[w].seg0, P, lane);
+      run_segment<LDS>(S, w, g - S.w[w].seg0, P, lane);
     }
   }
   __syncthreads();
@@ -402,6 +484,7 @@ __device__ int argmax_or_mark(Smem& S, int first, int count, double prior_val) {
 }
 
 // search_maxalpha for the points in slots [p0, p0+np) (sm-search.c:269-300)
+template <bool LDS>
 __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < np) set_binade(S.pt[p0 + tid]);
@@ -416,7 +499,7 @@ __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
   if (tid == 0) { S.nwalk = np * P.n_coarse; S.cnt[3] += np; }
   __syncthreads();
   for (int phase = 0; phase < 2; phase++) {
-    eval_walks(S, P);
+    eval_walks<LDS>(S, P);
     // argmax per point, with slow-path settling
     for (int round = 0; round < 2; round++) {
       if (tid == 0) {
@@ -438,7 +521,7 @@ __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
       const int nwk = __builtin_amdgcn_readfirstlane(S.nwalk);
       for (int w = wave; w < nwk; w += NWAVE) {
         if (__builtin_amdgcn_readfirstlane(S.need_slow[w])) {
-          const double v = walk_sequential(S.w[w], S.pt[S.w[w].p], P, lane);
+          const double v = walk_sequential<LDS>(S, S.w[w], S.pt[S.w[w].p], P, lane);
           if (lane == 0) { S.val[w] = v; S.exact[w] = 1; S.need_slow[w] = 0; atomicAdd(&S.cnt[5], 1ull); }
         }
       }
@@ -485,6 +568,7 @@ __device__ void write_point(fsclg_point_t& o, const Pt& pt) {
   o.lalpha = pt.la; o.null_logl = pt.N; o.sm_logl = pt.sm; o.clr = pt.clr;
 }
 
+template <bool LDS>
 __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
   __shared__ Smem S;
   const int tid = threadIdx.x;
@@ -494,6 +578,11 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
   const int cell = (nb % 8 == 0) ? x * per + slot : b;  // grids are launched as multiples of 8
   if (cell >= P.n_cells) return;
   if (tid < 8) S.cnt[tid] = 0;
+  if constexpr (LDS) {
+    for (int j = tid; j <= P.n_iv; j += WG) S.thr[j] = P.thr[j];
+    for (int j = tid; j < P.n_rows; j += WG) S.nul[j] = P.nullrow[j];
+  }
+  __syncthreads();
   if (P.mode == 1) {
     if (tid == 0) {
       const fsclg_point_t& in = P.out[cell];
@@ -503,14 +592,14 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
     }
     __syncthreads();
     if (tid == 0) S.cnt[1] += (unsigned long long)S.pt[0].n_snps;
-    search_maxalpha_pts(S, P, 0, 1);
+    search_maxalpha_pts<LDS>(S, P, 0, 1);
     if (tid == 0) write_point(P.out[cell], S.pt[0]);
   } else {
     const fsclg_cell_t c = P.cells[cell];
     if (tid < 2) init_point(S.pt[tid], c.chr, tid == 0 ? c.start_pos : c.end_pos, P);
     __syncthreads();
     if (tid == 0) S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps);
-    search_maxalpha_pts(S, P, 0, 2);  // start and end points share the two phases
+    search_maxalpha_pts<LDS>(S, P, 0, 2);  // start and end points share the two phases
     int iter = 0;
     for (;;) {
       const int sp = S.pt[0].sweep, ep = S.pt[1].sweep;
@@ -521,7 +610,7 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
         S.cnt[1] += (unsigned long long)S.pt[2].n_snps;
       }
       __syncthreads();
-      search_maxalpha_pts(S, P, 2, 1);
+      search_maxalpha_pts<LDS>(S, P, 2, 1);
       if (tid == 0) {
         // scan-chromosome.c:116: compare exactly as written
         if ((S.pt[0].clr + S.pt[2].clr) >= (S.pt[1].clr + S.pt[2].clr)) S.pt[1] = S.pt[2];
@@ -551,6 +640,7 @@ struct fsclg_ctx {
   double* d_logt = nullptr;
   double* d_coef = nullptr;
   double* d_null = nullptr;
+  double* d_thr = nullptr;
   int n_rows = 0, n_iv = 0;
   double step = 0.0;
   // snps
@@ -599,6 +689,21 @@ static int upload(T** dst, const T* src, size_t n, hipStream_t s) {
   return FSCLG_OK;
 }
 
+// least double x with (int)((x - LOG_AD_MIN) / step) >= j (sm-spline.c:52), by bisection over the
+// ordered doubles; the host evaluates the reference's expression with IEEE division
+static long long dkey(double x) { long long b; memcpy(&b, &x, 8); return b < 0 ? -(b & 0x7fffffffffffffffll) : b; }
+static double dval(long long k) { long long b = k < 0 ? ((-k) | (long long)0x8000000000000000ull) : k; double x; memcpy(&x, &b, 8); return x; }
+static int ref_interval(double x, double step) { return (int)((x - LOG_AD_MIN) / step); }
+static double interval_threshold(int j, double step) {
+  long long lo = dkey(LOG_AD_MIN - 1.0), hi = dkey(LOG_AD_MAX + 64.0);
+  if (ref_interval(dval(hi), step) < j) return dval(hi);
+  while ((unsigned long long)hi - (unsigned long long)lo > 1) {  // invariant: f(lo) < j <= f(hi)
+    const long long m = lo + (long long)(((unsigned long long)hi - (unsigned long long)lo) / 2);
+    if (ref_interval(dval(m), step) >= j) hi = m; else lo = m;
+  }
+  return dval(hi);
+}
+
 extern "C" {
 
 const char* fsclg_last_error(void) { return g_err; }
@@ -630,7 +735,7 @@ int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_logt, c->d_coef, c->d_null, c->d_pos, c->d_row0, c->d_row, c->d_chr_start, c->d_chr_n,
+  void* ptrs[] = {c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pos, c->d_row0, c->d_row, c->d_chr_start, c->d_chr_n,
                   c->d_chr_null, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   hipEventDestroy(c->ev0);
@@ -646,8 +751,17 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
   if ((r = upload(&c->d_logt, log_table, 0x10000, c->stream))) return r;
-  if ((r = upload(&c->d_coef, coef, (size_t)n_rows * n_iv * 4, c->stream))) return r;
+  std::vector<double> tcoef((size_t)n_rows * n_iv * 4);  // [row][iv][4] -> [iv][row][4]
+  for (int rr = 0; rr < n_rows; rr++)
+    for (int iv = 0; iv < n_iv; iv++)
+      memcpy(&tcoef[((size_t)iv * n_rows + rr) * 4], coef + ((size_t)rr * n_iv + iv) * 4, sizeof(double) * 4);
+  if ((r = upload(&c->d_coef, tcoef.data(), tcoef.size(), c->stream))) return r;
   if ((r = upload(&c->d_null, nullrow, (size_t)n_rows, c->stream))) return r;
+  std::vector<double> thr((size_t)n_iv + 1, 0.0);
+  for (int j = 1; j < n_iv; j++) thr[j] = interval_threshold(j, log_ad_step);
+  thr[0] = -__builtin_inf();     // iv 0 never steps down
+  thr[n_iv] = __builtin_inf();   // iv n_iv-1 never steps up (the reference clamps)
+  if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->stream))) return r;
   c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
   return FSCLG_OK;
 }
@@ -715,6 +829,7 @@ static int ensure_io(fsclg_ctx* c, int n) {
 static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
   Params P;
   P.pos = c->d_pos; P.row = c->d_row; P.logt = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
+  P.thr = c->d_thr; P.n_rows = c->n_rows; P.inv_step = 1.0 / c->step;
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats;
@@ -726,7 +841,10 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
 static int launch(fsclg_ctx* c, const Params& P, int n) {
   HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
   const int grid = (n + 7) / 8 * 8;
-  hipLaunchKernelGGL(search_maxpos_kernel, dim3(grid), dim3(WG), 0, c->stream, P);
+  if (c->n_iv <= MAXIV && c->n_rows <= MAXROWS)
+    hipLaunchKernelGGL(search_maxpos_kernel<true>, dim3(grid), dim3(WG), 0, c->stream, P);
+  else
+    hipLaunchKernelGGL(search_maxpos_kernel<false>, dim3(grid), dim3(WG), 0, c->stream, P);
   HIPCHK(hipGetLastError(), "launch search_maxpos_kernel");
   HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
   return FSCLG_OK;
@@ -786,6 +904,13 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
   c->kernel_ms += ms;
   c->launches++;
+  return FSCLG_OK;
+}
+
+int fsclg_interval_thresholds(double log_ad_step, int n_iv, double* thr) {
+  if (!thr || n_iv <= 0 || !(log_ad_step > 0)) return set_err(FSCLG_E_ARG, "thresholds");
+  thr[0] = 0.0;
+  for (int j = 1; j <= n_iv; j++) thr[j] = interval_threshold(j, log_ad_step);
   return FSCLG_OK;
 }
 

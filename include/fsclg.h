@@ -103,6 +103,11 @@ int fsclg_search_maxpos(fsclg_ctx *c, const fsclg_cell_t *cells, int n_cells, in
    already set (init_scan_result done by the caller); fills lalpha/sm_logl/clr */
 int fsclg_search_points(fsclg_ctx *c, fsclg_point_t *pts, int n_pts);
 
+/* the exact interval thresholds the kernel uses in place of spline_interpolate's
+   division (sm-spline.c:52): thr[j] = least double x with
+   (int)((x - LOG_AD_MIN) / log_ad_step) >= j, for j = 1..n_iv (thr has n_iv+1 slots) */
+int fsclg_interval_thresholds(double log_ad_step, int n_iv, double *thr);
+
 int fsclg_get_stats(fsclg_ctx *c, fsclg_stats_t *st);
 int fsclg_reset_stats(fsclg_ctx *c);
 

@@ -228,3 +228,23 @@ def test_output_bs_and_no_scan(built, tmp):
                         f"--output-bs={tmp / 'bs2.txt'}"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert (tmp / "bs2.txt").read_text() == bs.read_text()
+
+
+@pytest.mark.parametrize("n_iv", [200, 257, 500])
+def test_interval_thresholds_reproduce_the_division(built, n_iv):
+    """The kernel picks spline intervals by multiply + exact thresholds instead of
+    sm-spline.c:52's division; the thresholds must reproduce the division exactly."""
+    L = fscl_amd.get_lib()
+    step = 24.0 / (n_iv + 1.0)
+    thr = (C.c_double * (n_iv + 1))()
+    assert L.fsclg_interval_thresholds(step, n_iv, thr) == 0
+    T = np.array(thr[:])
+    rng = np.random.default_rng(n_iv)
+    xs = np.concatenate([rng.uniform(-20.0, 4.0, 200_000), T[1:n_iv], np.nextafter(T[1:n_iv], -np.inf),
+                         np.nextafter(T[1:n_iv], np.inf), [-20.0, 4.0]])
+    ref = np.clip(((xs - -20.0) / step).astype(np.int64), 0, n_iv - 1)
+    iv = np.clip(((xs - -20.0) * (1.0 / step)).astype(np.int64), 0, n_iv - 1)
+    up = (iv + 1 < n_iv) & (xs >= T[np.minimum(iv + 1, n_iv)])
+    down = ~up & (iv > 0) & (xs < T[iv])
+    got = iv + up - down
+    assert np.array_equal(got, ref)
