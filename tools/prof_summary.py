@@ -1,0 +1,48 @@
+"""Summarize a tools/profile.sh run into profiles/<tag>_*.  Usage:
+    python tools/prof_summary.py gpurun_out/prof_<tag> profiles/<tag>
+Writes <tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats) and
+<tag>_summary.json (per-launch PMC averages of search_maxpos_kernel, HBM bytes
+with the gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md §HBM)."""
+import csv
+import json
+import shutil
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+src, dst = Path(sys.argv[1]), sys.argv[2]
+Path(dst).parent.mkdir(parents=True, exist_ok=True)
+shutil.copy(src / "trace" / "run_kernel_stats.csv", f"{dst}_kernel_stats.csv")
+out = {"kernel": "search_maxpos_kernel"}
+for row in csv.DictReader(open(src / "trace" / "run_kernel_stats.csv")):
+    if "search_maxpos" in row["Name"]:
+        out["trace"] = {"calls": int(row["Calls"]), "avg_ms": float(row["AverageNs"]) / 1e6,
+                        "min_ms": float(row["MinNs"]) / 1e6, "max_ms": float(row["MaxNs"]) / 1e6,
+                        "share_pct": float(row["Percentage"])}
+pmc = {}
+for grp in ("fetch", "write", "sq"):
+    f = src / grp / "run_counter_collection.csv"
+    if not f.exists():
+        continue
+    agg, n = defaultdict(float), defaultdict(int)
+    for r in csv.DictReader(open(f)):
+        if "search_maxpos" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+            n[r["Counter_Name"]] += 1
+    for k in agg:
+        pmc[k] = agg[k] / n[k]
+out["pmc_per_launch"] = pmc
+if "FETCH_SIZE" in pmc:
+    fetch = pmc["FETCH_SIZE"] * 1024 * 2  # KB; x2: gfx950 FETCH_SIZE counts half of wide coalesced reads
+    write = pmc.get("WRITE_SIZE", 0.0) * 1024
+    out["hbm_bytes_per_launch"] = fetch + write
+    out["hbm_bytes_note"] = "(FETCH_SIZE*2 + WRITE_SIZE) * 1024, MI355X_MICROARCH.md §HBM correction"
+for name in ("bench_trace.json", "bench_fetch.json"):
+    p = src / name
+    if p.exists() and p.read_text().strip():
+        b = json.loads(p.read_text().strip().splitlines()[-1])
+        out.setdefault("bench", {})[name] = {"avg_launch_ms_hip_events": b["roofline"]["avg_launch_ms"],
+                                             "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"],
+                                             "value": b["value"], "ms_per_step": b["ms_per_step"]}
+json.dump(out, open(f"{dst}_summary.json", "w"), indent=1)
+print(json.dumps(out, indent=1))
