@@ -64,10 +64,17 @@ def main() -> int:
     import fscl_amd
     from fscl_amd import synth
 
+    # FSCL_AMD_DEVICE / FSCL_BENCH_BACKEND=gloo: rehearse several ranks on one GPU (tests only)
+    device = int(os.environ.get("FSCL_AMD_DEVICE", local))
+    backend = os.environ.get("FSCL_BENCH_BACKEND", "nccl")
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        dev = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            dev = torch.device("cuda", device)
+        else:
+            dist.init_process_group(backend)
+            dev = torch.device("cpu")
 
         def allreduce(arr: np.ndarray) -> None:
             t = torch.from_numpy(arr).to(dev)
@@ -75,7 +82,7 @@ def main() -> int:
             arr[:] = t.cpu().numpy()
 
         fscl_amd.set_ranks(rank, world, allreduce)
-    fscl_amd.set_device(local)
+    fscl_amd.set_device(device)
 
     cfg = dict(synth.CONFIGS[args.config])
     n_permute = cfg["n_permute"] if args.n_permute is None else args.n_permute
