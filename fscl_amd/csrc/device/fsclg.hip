@@ -56,15 +56,17 @@ constexpr int MAXROWS = 2048;      // spline rows whose null_logl lives in LDS
 constexpr int U = FSCLG_U;         // terms per lane per loop trip (independent load chains)
 constexpr double LOG_AD_MIN = -20.0;  // fscl.h:79
 constexpr double LOG_AD_MAX = 4.0;    // fscl.h:80
+constexpr int PAD = 1024;             // slack after pos/row: a trip may read up to 64*U past a walk's end
+constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsigned order = signed order
 
 enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2 };
 
 struct Params {
-  const int32_t* pos;
-  const uint32_t* row;
-  const double* logt;
-  const double* coef;
-  const double* nullrow;
+  const uint32_t* upos;        // [n_snps + PAD] position ^ POS_BIAS
+  const uint32_t* row;         // [n_snps + PAD]
+  const double* logt3;         // [3][65536]: c_b + log_table[i], the three branches of sm-search.c:40-46
+  const double* coef;          // [n_iv][n_rows + 1][4], row n_rows all zero (sentinel)
+  const double* nullrow;       // [n_rows + 1], entry n_rows zero
   const double* thr;           // thr[j] = least x with (int)((x - LOG_AD_MIN) / step) >= j, j = 1..n_iv-1
   const int32_t* chr_start;
   const int32_t* chr_n;
@@ -78,8 +80,10 @@ struct Params {
   int n_coarse;
   int n_iv;
   int n_rows;
+  int stride;                  // n_rows + 1
   double step;
   double inv_step;
+  double iv_off;               // -LOG_AD_MIN * inv_step
   int eval_range;
   int bp_resl;
   int n_cells;
@@ -96,7 +100,7 @@ struct Walk {
   int nl, nr;     // terms left / right of the nearest SNP
   int len;        // 0 (nearest already outside log(ad) <= 4) or 1 + nl + nr
   int seg0;       // first global segment id
-  int nseg;
+  int nseg;       // left-part segments then right-part segments (seg_range)
   double la;
 };
 
@@ -123,26 +127,39 @@ struct Smem {
   double nul[MAXROWS];
 };
 
-__device__ __forceinline__ double logt_dev(int d, const double* __restrict__ LT) {
-  // sm-search.c:40-46, branch-free: one gather, then the same add (0.0 + x == x for x >= 0)
-  const int ad = d < 0 ? -d : d;
-  const bool b1 = ad > 0xFFFF, b2 = ad > 0xFFFFFF;
-  const int ix = b2 ? (ad >> 16) : (b1 ? (ad >> 8) : ad);
-  const double c = b2 ? 11.783502069519070 : (b1 ? 5.545177444479562 : 0.0);
-  return c + LT[ix];
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t i) {
+  // 32-bit byte offset from a scalar base (global_load saddr + voffset)
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(base) + (i << 2));
+}
+
+__device__ __forceinline__ int pos_at(const Params& P, int i) { return (int)(P.upos[i] ^ POS_BIAS); }
+
+// log of |d| as sm-search.c:40-46: three branches, each c_b + log_table[|d| >> 8b], merged
+// into one precomputed table (the host forms c_b + log_table[i] with the same IEEE add)
+__device__ __forceinline__ double logt_dev(uint32_t ad, const double* __restrict__ LT3) {
+  const uint32_t sh = ad > 0xFFFFFFu ? 16u : (ad > 0xFFFFu ? 8u : 0u);
+  const uint32_t ix = (ad >> sh) + (sh << 13);  // + 65536 * branch
+  return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(LT3) + (ix << 3));
+}
+
+// |pos_i - sweep| from biased positions: one v_sad_u32
+__device__ __forceinline__ uint32_t absdist(uint32_t upos, uint32_t usweep) {
+  uint32_t d;
+  asm("v_sad_u32 %0, %1, %2, 0" : "=v"(d) : "v"(upos), "v"(usweep));
+  return d;
 }
 
 __device__ __forceinline__ double log_ad_of(int i, int sweep, double la, const Params& P) {
-  return logt_dev(P.pos[i] - sweep, P.logt) + la;
+  return logt_dev(absdist(P.upos[i], (uint32_t)sweep ^ POS_BIAS), P.logt3) + la;
 }
 
 // spline interval of sm-spline.c:52-54, (int)((x - LOG_AD_MIN) / step) clamped, without the
-// division: a multiply estimate is within one of it, and exact thresholds settle it
+// division: an fma estimate is within one of it, and exact thresholds settle it
 // (thr[0] = -inf and thr[n_iv] = +inf make the correction branch-free)
 template <bool LDS>
 __device__ __forceinline__ int interval_of(double x, const Smem& S, const Params& P) {
-  int iv = (int)((x - LOG_AD_MIN) * P.inv_step);
-  iv = iv < 0 ? 0 : (iv >= P.n_iv ? P.n_iv - 1 : iv);
+  int iv = (int)__builtin_fma(x, P.inv_step, P.iv_off);
+  iv = min(max(iv, 0), P.n_iv - 1);
   double lo, hi;
   if constexpr (LDS) { lo = S.thr[iv]; hi = S.thr[iv + 1]; }
   else { lo = P.thr[iv]; hi = P.thr[iv + 1]; }
@@ -156,9 +173,11 @@ __device__ __forceinline__ double null_of(uint32_t r, const Smem& S, const Param
 }
 
 // coefficient block of (row, interval): interval-major [iv][row][4], so the lanes of a
-// wave (neighbouring sites, nearly equal log distance) read from one interval's rows
+// wave (neighbouring sites, nearly equal log distance) read from one interval's rows;
+// 32-bit byte offset (the table is < 4 GiB, checked on upload)
 __device__ __forceinline__ const double2* coef_of(uint32_t r, int iv, const Params& P) {
-  return reinterpret_cast<const double2*>(P.coef + ((size_t)(uint32_t)iv * (uint32_t)P.n_rows + r) * 4);
+  const uint32_t off = (__umul24((uint32_t)iv, (uint32_t)P.stride) + r) << 5;
+  return reinterpret_cast<const double2*>(reinterpret_cast<const char*>(P.coef) + off);
 }
 
 // snp_likelihood (sm-search.c:85-103) with spline_interpolate (sm-spline.c:48-60)
@@ -189,15 +208,15 @@ __device__ void init_point(Pt& pt, int chr, int pos, const Params& P) {
   int i = 0, j = n;
   while (j - i > 1) {  // search_snppos, scan-chromosome.c:39-56
     const int m = (i + j) / 2;
-    if (P.pos[a + m] < pos) i = m; else j = m;
+    if (pos_at(P, a + m) < pos) i = m; else j = m;
   }
   int near;
   if (j == n) near = n - 1;
-  else if ((long long)pos - P.pos[a + i] < (long long)P.pos[a + j] - pos) near = i;
+  else if ((long long)pos - pos_at(P, a + i) < (long long)pos_at(P, a + j) - pos) near = i;
   else near = j;
   near += a;
   // Q3: the de-collision loop compares a global index with the chromosome's count
-  for (int ii = near; ii < n && P.pos[ii] == pos; ii++) pos++;
+  for (int ii = near; ii < n && pos_at(P, ii) == pos; ii++) pos++;
   const int cs = a, ce = a + n - 1, er = P.eval_range;
   int ws, we;
   if (near - er < cs) {
@@ -272,106 +291,98 @@ __device__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, co
   return acc;
 }
 
-// one 1024-term segment of one walk, by one wave: U terms per lane per trip, the
-// loads of all U issued before any is consumed, no divergent branches except
-// the (rare) tie record.  Per lane: exact int64 sum of M = rne(t/u) and of its
-// negative part (the positive part is their difference).
+// segment s of a walk, in index order j = i - (nearest - nl): the left part (j <= nl, the
+// nearest SNP and those before it) owns segments [0, nsl), the right part the rest, so
+// each part's k-order (sm-search.c:190-228) is monotone in j within it
+__device__ __forceinline__ int left_segs(int nl) { return (nl + SEG) / SEG; }
+__device__ __forceinline__ void seg_range(const Walk& W, int s, int& jb, int& je) {
+  const int nsl = left_segs(W.nl);
+  if (s < nsl) { jb = s * SEG; je = min(jb + SEG, W.nl + 1); }
+  else { jb = W.nl + 1 + (s - nsl) * SEG; je = min(jb + SEG, W.len); }
+}
+
+// one segment (<= 1024 terms) of one walk, by one wave, in index order: U terms per
+// lane per trip with all loads issued first; lanes past the segment read the padding
+// and take the zero sentinel row (term exactly 0).  Per lane: R = rint(t/u) summed in
+// fp64 (exact: < 2^53, checked once per segment) together with sum |R|.
 template <bool LDS>
 __device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane) {
 #ifdef FSCLG_EXP_NOTERMS  // timing ablation only: skip every term
   return;
 #endif
-  const int near = S.pt[S.w[w].p].nearest, sweep = S.pt[S.w[w].p].sweep, nl = S.w[w].nl, len = S.w[w].len;
-  const double la = S.w[w].la, inv = S.pt[S.w[w].p].inv_u;
-  const double lim = fmin(4611686018427387904.0 / (double)(len > 0 ? len : 1), 1125899906842624.0);  // 2^62/len, 2^50
-  const double MAGIC = 6755399441055744.0;  // 1.5 * 2^52: integer-valued |v| < 2^51 -> int64 by a bit subtraction
-  const long long MAGIC_BITS = 0x4338000000000000ll;
-  const int k0 = s * SEG;
-  const int k1 = (k0 + SEG < len) ? k0 + SEG : len;
-  long long sum = 0, neg = 0;
-  int par = 0;
-  bool big = false;
-  for (int kb = k0; kb < k1; kb += 64 * U) {
-    int idx[U];
-    bool act[U];
-    int pv[U];
-    uint32_t rv[U];
+  const Walk& W = S.w[w];
+  const Pt& pt = S.pt[W.p];
+  const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS;
+  const double la = W.la, inv = pt.inv_u;
+  const uint32_t lo = (uint32_t)(pt.nearest - W.nl);
+  int jb, je;
+  seg_range(W, s, jb, je);
+  double sum = 0.0, mag = 0.0;
+  for (int kb = jb; kb < je; kb += 64 * U) {
+    uint32_t pv[U], rv[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int k = kb + 64 * u + lane;
-      act[u] = k < k1;
-      const int kk = act[u] ? k : 0;
-      idx[u] = kk <= nl ? near - kk : near + (kk - nl);
+      const uint32_t i = lo + (uint32_t)(kb + 64 * u + lane);
+      pv[u] = ld_u32(P.upos, i);
+      rv[u] = ld_u32(P.row, i);
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) { pv[u] = P.pos[idx[u]]; rv[u] = P.row[idx[u]]; }
+    for (int u = 0; u < U; u++)
+      if (kb + 64 * u + lane >= je) rv[u] = (uint32_t)P.n_rows;  // sentinel
     double x[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-#ifdef FSCLG_EXP_NOLT   // timing ablation only: no log-table gather
-      x[u] = (double)((pv[u] - sweep) & 15) + la;
-#else
-      x[u] = logt_dev(pv[u] - sweep, P.logt) + la;
-#endif
-    }
+    for (int u = 0; u < U; u++) x[u] = logt_dev(absdist(pv[u], usweep), P.logt3) + la;
     double2 ca[U], cb[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int iv = interval_of<LDS>(x[u], S, P);
-#ifdef FSCLG_EXP_NOCOEF  // timing ablation only: every lane reads one coefficient block
-      const double2* cp = reinterpret_cast<const double2*>(P.coef + (size_t)(iv & 1) * 4);
-#else
-      const double2* cp = coef_of(rv[u], iv, P);
-#endif
+      const double2* cp = coef_of(rv[u], interval_of<LDS>(x[u], S, P), P);
       ca[u] = cp[0];
       cb[u] = cp[1];
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
-      const double t = y - null_of<LDS>(rv[u], S, P);
-      const double q = t * inv;
-      const double F = floor(q);
-      const double fr = q - F;
-      const bool ok = fabs(q) < lim;
-      big |= act[u] & !ok;
-      const bool use = act[u] & ok;
-      const bool tie = use & (fr == 0.5);
-      const double Md = F + (fr > 0.5 ? 1.0 : 0.0);
-      const long long Mv = __double_as_longlong(Md + MAGIC) - MAGIC_BITS;
-      const long long M = use ? Mv : 0;
-      sum += M;
-      neg += M < 0 ? M : 0;
-      const unsigned long long low = __ballot((M & 1) != 0);
-      const unsigned long long tm = __ballot(tie);
-      if (tm) {
-        if (tie) {
-          const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-          const int pre = par ^ (__popcll(low & below) & 1);
+      const double q = (y - null_of<LDS>(rv[u], S, P)) * inv;
+      const double R = rint(q);                 // the even neighbour at a tie; the resolver settles ties
+      const double fr = q - R;
+      if (__ballot(fabs(fr) == 0.5)) {          // rare: record the tie with its in-segment prefix parity
+        const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        const unsigned long long ps = __ballot(sum - 2.0 * floor(0.5 * sum) != 0.0);
+        const unsigned long long pr = __ballot(R - 2.0 * floor(0.5 * R) != 0.0);
+        if (fabs(fr) == 0.5) {
+          const int pre = (__popcll(ps) + __popcll(pr & below)) & 1;
           const int ti = atomicAdd(&S.n_ties, 1);
-          if (ti < MAXTIES) S.ties[ti] = (w << 20) | ((int)(M & 1) << 19) | (pre << 18) | (kb + 64 * u + lane);
+          if (ti < MAXTIES) S.ties[ti] = (w << 20) | ((fr < 0.0 ? 1 : 0) << 19) | (pre << 18) | (kb + 64 * u + lane);
         }
       }
-      par ^= __popcll(low) & 1;
+      sum += R;
+      mag += fabs(R);
     }
   }
-  sum = wave_sum64(sum);
-  neg = wave_sum64(neg);
+  // exactness: every partial of |R| below 2^53 (fl is monotone, so fl(mag) < 2^53 says so,
+  // NaN fails it), and the walk's int64 totals below 2^61
+  const double limA = fmin(9007199254740992.0, 36028797018963968.0 / (double)W.nseg);  // 2^53, 2^55/nseg
+  const bool big = !(mag < limA);
+  const long long isum = wave_sum64((long long)sum);
+  const long long imag = wave_sum64((long long)mag);
   const bool anybig = __any(big);
   if (lane == 0) {
-    atomicAdd(&S.P[w], (unsigned long long)(sum - neg));
-    atomicAdd(&S.Q[w], (unsigned long long)neg);
-    if (par) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
+    atomicAdd(&S.P[w], (unsigned long long)isum);
+    atomicAdd(&S.Q[w], (unsigned long long)imag);
+    if (isum & 1) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
     if (anybig) atomicOr(&S.wflag[w], 1);
   }
 }
 
-// resolve walk w's exact value (thread per walk)
+// resolve walk w's exact value (thread per walk).  S.P = sum R, S.Q = sum |R| over the walk.
+// Ties are replayed in k order: fl(acc + t) rounds to even, so where t/u = F + 1/2 an odd
+// running sum takes the other neighbour of the even R (+1 if R = F, -1 if R = F + 1).
 __device__ void resolve_walk(Smem& S, int w) {
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[W.p];
   if (W.len == 0) { S.exact[w] = 1; S.val[w] = pt.N; return; }
-  const long long P = (long long)S.P[w], Q = (long long)S.Q[w];
+  const long long Ssum = (long long)S.P[w], A = (long long)S.Q[w];
+  const long long Pp = (Ssum + A) / 2, Qn = (Ssum - A) / 2;   // positive / negative parts
   const bool overflow = S.n_ties > MAXTIES;
   int T = 0;
   const int nt = S.n_ties < MAXTIES ? S.n_ties : MAXTIES;
@@ -379,28 +390,38 @@ __device__ void resolve_walk(Smem& S, int w) {
   const bool big = S.wflag[w] != 0 || pt.inv_u == 0.0;
   const long long S0 = big ? 0 : (long long)(pt.N * pt.inv_u);
   const long long LO = -(1ll << 53), HI = -((1ll << 52) + 1);
-  const bool safe = !big && !overflow && S0 < 0 && (S0 + Q >= LO) && (S0 + P + T <= HI);
+  const bool safe = !big && !overflow && S0 < 0 && (S0 + Qn - T >= LO) && (S0 + Pp + T <= HI);
   if (safe) {
-    int cumpar = (int)(S0 & 1), cs = 0, adjx = 0;
+    const int nl = W.nl, nsl = left_segs(nl);
+    auto segbit = [&](int sg) { return (int)(S.segbits[w][sg >> 5] >> (sg & 31)) & 1; };
+    int lpar = 0;
+    for (int sg = 0; sg < nsl; sg++) lpar ^= segbit(sg);
+    int adjx = 0;
     long long adjs = 0;
     int prevk = -1;
     for (int c = 0; c < T; c++) {  // ties of this walk in k order
       int bestk = 0x7fffffff, bestv = 0;
       for (int j = 0; j < nt; j++) {
         const int v = S.ties[j];
-        const int k = v & 0x3FFFF;
+        const int jj = v & 0x3FFFF;
+        const int k = jj <= nl ? nl - jj : jj;
         if ((v >> 20) == w && k > prevk && k < bestk) { bestk = k; bestv = v; }
       }
       prevk = bestk;
-      const int s = bestk / SEG;
-      while (cs < s) { cumpar ^= (S.segbits[w][cs >> 5] >> (cs & 31)) & 1; cs++; }
-      const int pre = (bestv >> 18) & 1, fpar = (bestv >> 19) & 1;
-      const int adj = cumpar ^ pre ^ adjx ^ fpar;
+      // parity of the running sum before this term: S0, then the terms before it in k
+      // order = (left tie) the left part after it, (right tie) the left part and the
+      // right part before it; R of a tie is even, so both read lpar ^ prefix-in-part
+      const int jj = bestv & 0x3FFFF;
+      const int sg = jj <= nl ? jj / SEG : nsl + (jj - nl - 1) / SEG;
+      int sp = 0;
+      for (int t = (jj <= nl ? 0 : nsl); t < sg; t++) sp ^= segbit(t);
+      const int pre = (bestv >> 18) & 1, up = (bestv >> 19) & 1;
+      const int adj = (int)(S0 & 1) ^ lpar ^ sp ^ pre ^ adjx;
       adjx ^= adj;
-      adjs += adj;
+      adjs += adj ? (up ? -1 : 1) : 0;
     }
     S.exact[w] = 1;
-    S.val[w] = (double)(S0 + P + Q + adjs) * pt.u;
+    S.val[w] = (double)(S0 + Ssum + adjs) * pt.u;
   } else {
     S.exact[w] = 0;
     if (big) {
@@ -408,8 +429,8 @@ __device__ void resolve_walk(Smem& S, int w) {
       S.bnd[w] = 0.0;
     } else {
       const double u = pt.u, len = (double)W.len;
-      const double smax = fabs(pt.N) + ((double)P - (double)Q + len) * u;
-      S.appr[w] = (double)(S0 + P + Q) * u;
+      const double smax = fabs(pt.N) + ((double)A + len) * u;
+      S.appr[w] = (double)(S0 + Ssum) * u;
       S.bnd[w] = 2.0 * (len * u + len * 4.440892098500626e-16 * smax) + 1e-300;
     }
     atomicAdd(&S.cnt[4], 1ull);
@@ -435,7 +456,7 @@ __device__ void eval_walks(Smem& S, const Params& P) {
     for (int w = 0; w < nw; w++) {
       Walk& W = S.w[w];
       W.len = W.len ? 1 + W.nl + W.nr : 0;
-      W.nseg = (W.len + SEG - 1) / SEG;
+      W.nseg = W.len ? left_segs(W.nl) + (W.nr + SEG - 1) / SEG : 0;
       W.seg0 = seg;
       seg += W.nseg;
       terms += W.len;
@@ -580,7 +601,7 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
   if (tid < 8) S.cnt[tid] = 0;
   if constexpr (LDS) {
     for (int j = tid; j <= P.n_iv; j += WG) S.thr[j] = P.thr[j];
-    for (int j = tid; j < P.n_rows; j += WG) S.nul[j] = P.nullrow[j];
+    for (int j = tid; j <= P.n_rows; j += WG) S.nul[j] = P.nullrow[j];  // + sentinel
   }
   __syncthreads();
   if (P.mode == 1) {
@@ -644,7 +665,7 @@ struct fsclg_ctx {
   int n_rows = 0, n_iv = 0;
   double step = 0.0;
   // snps
-  int32_t* d_pos = nullptr;
+  uint32_t* d_pos = nullptr;      // biased positions, n_snps + PAD
   uint32_t* d_row0 = nullptr;
   uint32_t* d_row = nullptr;
   int n_snps = 0;
@@ -748,15 +769,30 @@ int fsclg_close(fsclg_ctx* c) {
 int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coef, int n_rows, int n_iv,
                         const double* nullrow, double log_ad_step) {
   if (!c || !log_table || !coef || !nullrow || n_rows <= 0 || n_iv <= 0) return set_err(FSCLG_E_ARG, "tables");
+  if ((unsigned long long)(n_rows + 1) * (unsigned long long)n_iv * 32ull >= (1ull << 32))
+    return set_err(FSCLG_E_ARG, "coefficient table exceeds 4 GiB (32-bit offsets)");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
-  if ((r = upload(&c->d_logt, log_table, 0x10000, c->stream))) return r;
-  std::vector<double> tcoef((size_t)n_rows * n_iv * 4);  // [row][iv][4] -> [iv][row][4]
+  // the three branches of sm-search.c:40-46 (c_b + log_table[i]) as one table; the same
+  // IEEE double add as the reference's, so every entry is bit-identical to its result
+  std::vector<double> lt3(3 * 0x10000);
+  const double cb[3] = {0.0, 5.545177444479562, 11.783502069519070};
+  for (int b = 0; b < 3; b++)
+    for (int i = 0; i < 0x10000; i++) {
+      volatile double v = cb[b] + log_table[i];
+      lt3[(size_t)b * 0x10000 + i] = b ? (double)v : log_table[i];
+    }
+  if ((r = upload(&c->d_logt, lt3.data(), lt3.size(), c->stream))) return r;
+  // [row][iv][4] -> [iv][row][4], plus an all-zero sentinel row n_rows (terms exactly 0)
+  const size_t stride = (size_t)n_rows + 1;
+  std::vector<double> tcoef(stride * n_iv * 4, 0.0);
   for (int rr = 0; rr < n_rows; rr++)
     for (int iv = 0; iv < n_iv; iv++)
-      memcpy(&tcoef[((size_t)iv * n_rows + rr) * 4], coef + ((size_t)rr * n_iv + iv) * 4, sizeof(double) * 4);
+      memcpy(&tcoef[((size_t)iv * stride + rr) * 4], coef + ((size_t)rr * n_iv + iv) * 4, sizeof(double) * 4);
   if ((r = upload(&c->d_coef, tcoef.data(), tcoef.size(), c->stream))) return r;
-  if ((r = upload(&c->d_null, nullrow, (size_t)n_rows, c->stream))) return r;
+  std::vector<double> nul(nullrow, nullrow + n_rows);
+  nul.push_back(0.0);
+  if ((r = upload(&c->d_null, nul.data(), nul.size(), c->stream))) return r;
   std::vector<double> thr((size_t)n_iv + 1, 0.0);
   for (int j = 1; j < n_iv; j++) thr[j] = interval_threshold(j, log_ad_step);
   thr[0] = -__builtin_inf();     // iv 0 never steps down
@@ -775,9 +811,12 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
     if (c->n_rows && row[i] >= (uint32_t)c->n_rows) return set_err(FSCLG_E_ARG, "row index out of table");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
-  if ((r = upload(&c->d_pos, pos, (size_t)n_snps, c->stream))) return r;
-  if ((r = upload(&c->d_row0, row, (size_t)n_snps, c->stream))) return r;
-  if ((r = upload(&c->d_row, row, (size_t)n_snps, c->stream))) return r;
+  // PAD slack after both arrays (zeros: a valid position and row, never counted)
+  std::vector<uint32_t> up((size_t)n_snps + PAD, POS_BIAS), ur((size_t)n_snps + PAD, 0u);
+  for (int i = 0; i < n_snps; i++) { up[i] = (uint32_t)pos[i] ^ POS_BIAS; ur[i] = row[i]; }
+  if ((r = upload(&c->d_pos, up.data(), up.size(), c->stream))) return r;
+  if ((r = upload(&c->d_row0, ur.data(), ur.size(), c->stream))) return r;
+  if ((r = upload(&c->d_row, ur.data(), ur.size(), c->stream))) return r;
   if ((r = upload(&c->d_chr_start, chr_start, (size_t)n_chr, c->stream))) return r;
   if ((r = upload(&c->d_chr_n, chr_n, (size_t)n_chr, c->stream))) return r;
   if ((r = upload<double>(&c->d_chr_null, nullptr, (size_t)n_chr, c->stream))) return r;
@@ -828,8 +867,9 @@ static int ensure_io(fsclg_ctx* c, int n) {
 
 static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
   Params P;
-  P.pos = c->d_pos; P.row = c->d_row; P.logt = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
-  P.thr = c->d_thr; P.n_rows = c->n_rows; P.inv_step = 1.0 / c->step;
+  P.upos = c->d_pos; P.row = c->d_row; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
+  P.thr = c->d_thr; P.n_rows = c->n_rows; P.stride = c->n_rows + 1;
+  P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step;
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats;
@@ -841,7 +881,7 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
 static int launch(fsclg_ctx* c, const Params& P, int n) {
   HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
   const int grid = (n + 7) / 8 * 8;
-  if (c->n_iv <= MAXIV && c->n_rows <= MAXROWS)
+  if (c->n_iv <= MAXIV && c->n_rows + 1 <= MAXROWS)
     hipLaunchKernelGGL(search_maxpos_kernel<true>, dim3(grid), dim3(WG), 0, c->stream, P);
   else
     hipLaunchKernelGGL(search_maxpos_kernel<false>, dim3(grid), dim3(WG), 0, c->stream, P);
