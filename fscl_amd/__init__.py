@@ -74,7 +74,9 @@ class Stats(C.Structure):  # fscl_amd_stats_t
                 ("kernel_ms", C.c_double), ("gp_evals", C.c_ulonglong), ("n_terms", C.c_ulonglong),
                 ("n_null", C.c_ulonglong), ("n_walks", C.c_ulonglong), ("n_maxalpha", C.c_ulonglong),
                 ("n_unsafe", C.c_ulonglong), ("n_slow", C.c_ulonglong), ("n_ties", C.c_ulonglong),
-                ("n_launches", C.c_ulonglong), ("negj", C.c_ulonglong), ("trials", C.c_int)]
+                ("n_launches", C.c_ulonglong), ("negj", C.c_ulonglong), ("trials", C.c_int),
+                ("cache_iv0", C.c_int), ("cache_n_iv", C.c_int), ("cache_n_rows", C.c_int),
+                ("cache_cover", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

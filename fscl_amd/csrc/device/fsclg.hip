@@ -25,8 +25,11 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <vector>
+#include <algorithm>
+#include <unordered_map>
 
 #include "../../../include/fsclg.h"
 
@@ -40,7 +43,13 @@
 
 namespace {
 
-constexpr int WG = 512;
+#ifndef FSCLG_WG
+#define FSCLG_WG 512
+#endif
+#ifndef FSCLG_LDS_WG
+#define FSCLG_LDS_WG 81920
+#endif
+constexpr int WG = FSCLG_WG;
 constexpr int NWAVE = WG / 64;
 constexpr int SEG = 1024;          // terms per work segment
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
@@ -48,8 +57,7 @@ constexpr int MAXSEG_W = 192;      // segments per walk (161 at 163841 terms)
 constexpr int SEGWORDS = MAXSEG_W / 32;
 constexpr int MAXTIES = 2048;
 constexpr int MAXREF = 16;
-constexpr int MAXIV = 1024;        // spline intervals whose thresholds live in LDS
-constexpr int MAXROWS = 2048;      // spline rows whose null_logl lives in LDS
+constexpr int LDS_WG = FSCLG_LDS_WG;  // LDS per workgroup (default: two workgroups per CU, 160 KiB)
 #ifndef FSCLG_U
 #define FSCLG_U 4
 #endif
@@ -63,10 +71,10 @@ enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2 };
 
 struct Params {
   const uint32_t* upos;        // [n_snps + PAD] position ^ POS_BIAS
-  const uint32_t* row;         // [n_snps + PAD]
+  const uint32_t* row;         // [n_snps + PAD] device row = caller's row + 1 (0: the zero sentinel)
   const double* logt3;         // [3][65536]: c_b + log_table[i], the three branches of sm-search.c:40-46
-  const double* coef;          // [n_iv][n_rows + 1][4], row n_rows all zero (sentinel)
-  const double* nullrow;       // [n_rows + 1], entry n_rows zero
+  const double* coef;          // [n_iv][n_rows + 1][4], device row 0 all zero (sentinel)
+  const double* nullrow;       // [n_rows + 1], entry 0 zero
   const double* thr;           // thr[j] = least x with (int)((x - LOG_AD_MIN) / step) >= j, j = 1..n_iv-1
   const int32_t* chr_start;
   const int32_t* chr_n;
@@ -77,6 +85,7 @@ struct Params {
   const fsclg_cell_t* cells;
   fsclg_point_t* out;
   unsigned long long* stats;   // 8 counters
+  unsigned long long* ctrace;  // optional per-cell [start, end, cu id, terms] (FSCLG_CELL_TRACE)
   int n_coarse;
   int n_iv;
   int n_rows;
@@ -84,6 +93,10 @@ struct Params {
   double step;
   double inv_step;
   double iv_off;               // -LOG_AD_MIN * inv_step
+  int ivc0;                    // LDS coefficient cache: intervals [ivc0, ivc0 + n_civ) x device rows [0, n_crow)
+  int n_civ, n_crow;
+  int n_cache;                 // n_civ * n_crow blocks
+  int off_b, off_thr, off_nul; // byte offsets in fsclg_dyn (plane A at 0)
   int eval_range;
   int bp_resl;
   int n_cells;
@@ -123,9 +136,11 @@ struct Smem {
   int n_slow;
   int best[3];
   unsigned long long cnt[8];
-  double thr[MAXIV + 1];
-  double nul[MAXROWS];
 };
+
+// dynamic LDS of a workgroup (LDS = true): coefficient planes of the top K intervals, the
+// interval thresholds and the null rows (offsets in Params)
+extern __shared__ __attribute__((aligned(16))) char fsclg_dyn[];
 
 __device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t i) {
   // 32-bit byte offset from a scalar base (global_load saddr + voffset)
@@ -161,14 +176,17 @@ __device__ __forceinline__ int interval_of(double x, const Smem& S, const Params
   int iv = (int)__builtin_fma(x, P.inv_step, P.iv_off);
   iv = min(max(iv, 0), P.n_iv - 1);
   double lo, hi;
-  if constexpr (LDS) { lo = S.thr[iv]; hi = S.thr[iv + 1]; }
+  if constexpr (LDS) {
+    const double* t = reinterpret_cast<const double*>(fsclg_dyn + P.off_thr);
+    lo = t[iv]; hi = t[iv + 1];
+  }
   else { lo = P.thr[iv]; hi = P.thr[iv + 1]; }
   return iv + (x >= hi ? 1 : 0) - (x < lo ? 1 : 0);
 }
 
 template <bool LDS>
 __device__ __forceinline__ double null_of(uint32_t r, const Smem& S, const Params& P) {
-  if constexpr (LDS) return S.nul[r];
+  if constexpr (LDS) return reinterpret_cast<const double*>(fsclg_dyn + P.off_nul)[r];
   else return P.nullrow[r];
 }
 
@@ -180,14 +198,93 @@ __device__ __forceinline__ const double2* coef_of(uint32_t r, int iv, const Para
   return reinterpret_cast<const double2*>(reinterpret_cast<const char*>(P.coef) + off);
 }
 
+// the coefficient block of (row, interval) into a = (c0, c1), b = (c2, c3): from the LDS
+// planes when (interval, row) lies in the cached window (planned on the host from sampled
+// walks and row frequencies, fsclg_plan_cache), from the global table otherwise
+template <bool LDS>
+__device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Params& P, double2& a, double2& b) {
+#ifdef FSCLG_NOCACHE  // experiment: coefficients always from the global table
+  if constexpr (false) {
+#else
+  if constexpr (LDS) {
+#endif
+    const uint32_t ci = (uint32_t)(iv - P.ivc0);
+    const bool hit = ci < (uint32_t)P.n_civ && r < (uint32_t)P.n_crow;
+    const uint32_t li = __umul24(min(ci, (uint32_t)P.n_civ - 1), (uint32_t)P.n_crow) + min(r, (uint32_t)P.n_crow - 1);
+    a = reinterpret_cast<const double2*>(fsclg_dyn)[li];
+    b = reinterpret_cast<const double2*>(fsclg_dyn + P.off_b)[li];
+    if (!hit) {
+      const double2* cp = coef_of(r, iv, P);
+      a = cp[0];
+      b = cp[1];
+    }
+  } else {
+    const double2* cp = coef_of(r, iv, P);
+    a = cp[0];
+    b = cp[1];
+  }
+}
+
+// coefficients of U terms, in stages so the loads of all U overlap: interval estimates and
+// their threshold reads, the corrections, the LDS reads, then one wave-uniform branch that
+// gathers the misses from the global table into separate registers and selects them
+template <bool LDS>
+__device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t (&rv)[U], const Smem& S,
+                                           const Params& P, double2 (&ca)[U], double2 (&cb)[U]) {
+#ifdef FSCLG_NOCACHE
+  constexpr bool CACHE = false;
+#else
+  constexpr bool CACHE = LDS;
+#endif
+  int iv[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) iv[u] = interval_of<LDS>(x[u], S, P);
+  if constexpr (CACHE) {
+    bool hit[U];
+    bool miss = false;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t ci = (uint32_t)(iv[u] - P.ivc0);
+      hit[u] = ci < (uint32_t)P.n_civ && rv[u] < (uint32_t)P.n_crow;
+      miss |= !hit[u];
+      const uint32_t li = __umul24(min(ci, (uint32_t)P.n_civ - 1), (uint32_t)P.n_crow) + min(rv[u], (uint32_t)P.n_crow - 1);
+      ca[u] = reinterpret_cast<const double2*>(fsclg_dyn)[li];
+      cb[u] = reinterpret_cast<const double2*>(fsclg_dyn + P.off_b)[li];
+    }
+    if (__ballot(miss)) {
+      double2 ga[U], gb[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const double2* cp = coef_of(rv[u], iv[u], P);
+        ga[u] = cp[0];
+        gb[u] = cp[1];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {  // component selects (a double2 ternary becomes a stack-address select)
+        ca[u].x = hit[u] ? ca[u].x : ga[u].x;
+        ca[u].y = hit[u] ? ca[u].y : ga[u].y;
+        cb[u].x = hit[u] ? cb[u].x : gb[u].x;
+        cb[u].y = hit[u] ? cb[u].y : gb[u].y;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const double2* cp = coef_of(rv[u], iv[u], P);
+      ca[u] = cp[0];
+      cb[u] = cp[1];
+    }
+  }
+}
+
 // snp_likelihood (sm-search.c:85-103) with spline_interpolate (sm-spline.c:48-60)
 template <bool LDS>
 __device__ __forceinline__ double term_dev(int i, int sweep, double la, const Smem& S, const Params& P) {
   const double x = log_ad_of(i, sweep, la, P);
   const int iv = interval_of<LDS>(x, S, P);
   const uint32_t r = P.row[i];
-  const double2* cp = coef_of(r, iv, P);
-  const double2 a = cp[0], b = cp[1];
+  double2 a, b;
+  coef_fetch<LDS>(r, iv, P, a, b);
   const double y = x * (a.x * x * x + a.y * x + b.x) + b.y;
   return y - null_of<LDS>(r, S, P);
 }
@@ -328,17 +425,12 @@ __device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane) {
     }
 #pragma unroll
     for (int u = 0; u < U; u++)
-      if (kb + 64 * u + lane >= je) rv[u] = (uint32_t)P.n_rows;  // sentinel
+      if (kb + 64 * u + lane >= je) rv[u] = 0u;  // zero sentinel row
     double x[U];
 #pragma unroll
     for (int u = 0; u < U; u++) x[u] = logt_dev(absdist(pv[u], usweep), P.logt3) + la;
     double2 ca[U], cb[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const double2* cp = coef_of(rv[u], interval_of<LDS>(x[u], S, P), P);
-      ca[u] = cp[0];
-      cb[u] = cp[1];
-    }
+    coef_stage<LDS>(x, rv, S, P, ca, cb);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
@@ -585,7 +677,7 @@ __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
 
 __device__ void write_point(fsclg_point_t& o, const Pt& pt) {
   o.chr = pt.chr; o.nearest_snp = pt.nearest; o.sweep_pos = pt.sweep; o.n_snps = pt.n_snps;
-  o.window_start = pt.wstart; o.window_end = pt.wend; o.flags = pt.flags; o.pad = 0;
+  o.window_start = pt.wstart; o.window_end = pt.wend; o.flags = pt.flags; o.cost = 0;
   o.lalpha = pt.la; o.null_logl = pt.N; o.sm_logl = pt.sm; o.clr = pt.clr;
 }
 
@@ -594,14 +686,26 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
   __shared__ Smem S;
   const int tid = threadIdx.x;
   // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous run of cells
-  const int nb = gridDim.x, b = blockIdx.x;
-  const int per = nb / 8, x = b % 8, slot = b / 8;
-  const int cell = (nb % 8 == 0) ? x * per + slot : b;  // grids are launched as multiples of 8
+  // cells arrive in the host's longest-first order; the hardware dispatches blocks in order
+  // (round-robin over the XCDs), so the long cells start first and spread over the XCDs
+  const int cell = blockIdx.x;
   if (cell >= P.n_cells) return;
   if (tid < 8) S.cnt[tid] = 0;
+  if (P.ctrace && tid == 0) { P.ctrace[4 * cell] = wall_clock64(); P.ctrace[4 * cell + 2] = __smid(); }
   if constexpr (LDS) {
-    for (int j = tid; j <= P.n_iv; j += WG) S.thr[j] = P.thr[j];
-    for (int j = tid; j <= P.n_rows; j += WG) S.nul[j] = P.nullrow[j];  // + sentinel
+    double* thr = reinterpret_cast<double*>(fsclg_dyn + P.off_thr);
+    double* nul = reinterpret_cast<double*>(fsclg_dyn + P.off_nul);
+    double2* ca = reinterpret_cast<double2*>(fsclg_dyn);
+    double2* cb = reinterpret_cast<double2*>(fsclg_dyn + P.off_b);
+    for (int j = tid; j <= P.n_iv; j += WG) thr[j] = P.thr[j];
+    for (int j = tid; j <= P.n_rows; j += WG) nul[j] = P.nullrow[j];  // + sentinel
+    // planes [ci][row] of the cached window
+    for (int e = tid; e < P.n_cache; e += WG) {
+      const int ci = e / P.n_crow, r = e - ci * P.n_crow;
+      const double2* src = reinterpret_cast<const double2*>(P.coef) + ((size_t)(P.ivc0 + ci) * P.stride + r) * 2;
+      ca[e] = src[0];
+      cb[e] = src[1];
+    }
   }
   __syncthreads();
   if (P.mode == 1) {
@@ -643,11 +747,13 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
       const Pt& r = S.pt[0].clr > S.pt[1].clr ? S.pt[0] : S.pt[1];
       write_point(P.out[cell], r);
       P.out[cell].flags |= S.pt[0].flags | S.pt[1].flags;
+      P.out[cell].cost = (uint32_t)min(S.cnt[0] >> 10, 0xFFFFFFFFull);
       S.cnt[7] += 1;
     }
   }
   __syncthreads();
   if (tid < 8 && S.cnt[tid]) atomicAdd(&P.stats[tid], S.cnt[tid]);
+  if (P.ctrace && tid == 0) { P.ctrace[4 * cell + 1] = wall_clock64(); P.ctrace[4 * cell + 3] = S.cnt[0]; }
 }
 
 }  // namespace
@@ -674,7 +780,17 @@ struct fsclg_ctx {
   double* d_chr_null = nullptr;
   int n_chr = 0;
   std::vector<int> h_chr_n;
+  std::vector<int32_t> h_pos, h_chr_start;
+  std::vector<long long> h_row_cnt;     // sites per device row
+  std::vector<double> h_lt3;
+  std::vector<uint32_t> h_stage;
+  // LDS coefficient cache plan (fsclg_plan_cache)
+  bool plan_dirty = true;
+  int c_ivc0 = 0, c_civ = 0, c_crow = 0;
+  double c_cover = 0.0;
   // alpha grid
+  std::vector<double> h_coarse, h_refine;
+  std::vector<int32_t> h_nref;
   double* d_la_coarse = nullptr;
   double* d_la_refine = nullptr;
   int32_t* d_n_refine = nullptr;
@@ -684,6 +800,12 @@ struct fsclg_ctx {
   fsclg_point_t* d_out = nullptr;
   int cap = 0;
   unsigned long long* d_stats = nullptr;
+  std::unordered_map<unsigned long long, uint32_t> cell_cost;  // (chr, start, end) -> cost of its last run
+  std::vector<fsclg_cell_t> h_cells;
+  std::vector<int> h_order;
+  std::vector<fsclg_point_t> h_out;
+  unsigned long long* d_ctrace = nullptr;  // FSCLG_CELL_TRACE=<file>: per-cell timing appended per launch
+  int ctrace_cap = 0;
   double kernel_ms = 0.0;
   unsigned long long launches = 0;
 };
@@ -756,7 +878,7 @@ int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pos, c->d_row0, c->d_row, c->d_chr_start, c->d_chr_n,
+  void* ptrs[] = {c->d_ctrace, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pos, c->d_row0, c->d_row, c->d_chr_start, c->d_chr_n,
                   c->d_chr_null, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   hipEventDestroy(c->ev0);
@@ -783,15 +905,16 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
       lt3[(size_t)b * 0x10000 + i] = b ? (double)v : log_table[i];
     }
   if ((r = upload(&c->d_logt, lt3.data(), lt3.size(), c->stream))) return r;
-  // [row][iv][4] -> [iv][row][4], plus an all-zero sentinel row n_rows (terms exactly 0)
+  c->h_lt3.swap(lt3);
+  // [row][iv][4] -> [iv][1 + row][4]: device row 0 is an all-zero sentinel (terms exactly 0)
   const size_t stride = (size_t)n_rows + 1;
   std::vector<double> tcoef(stride * n_iv * 4, 0.0);
   for (int rr = 0; rr < n_rows; rr++)
     for (int iv = 0; iv < n_iv; iv++)
-      memcpy(&tcoef[((size_t)iv * stride + rr) * 4], coef + ((size_t)rr * n_iv + iv) * 4, sizeof(double) * 4);
+      memcpy(&tcoef[((size_t)iv * stride + rr + 1) * 4], coef + ((size_t)rr * n_iv + iv) * 4, sizeof(double) * 4);
   if ((r = upload(&c->d_coef, tcoef.data(), tcoef.size(), c->stream))) return r;
-  std::vector<double> nul(nullrow, nullrow + n_rows);
-  nul.push_back(0.0);
+  std::vector<double> nul(1, 0.0);
+  nul.insert(nul.end(), nullrow, nullrow + n_rows);
   if ((r = upload(&c->d_null, nul.data(), nul.size(), c->stream))) return r;
   std::vector<double> thr((size_t)n_iv + 1, 0.0);
   for (int j = 1; j < n_iv; j++) thr[j] = interval_threshold(j, log_ad_step);
@@ -799,6 +922,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   thr[n_iv] = __builtin_inf();   // iv n_iv-1 never steps up (the reference clamps)
   if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->stream))) return r;
   c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
+  c->plan_dirty = true;
   return FSCLG_OK;
 }
 
@@ -813,7 +937,7 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   int r;
   // PAD slack after both arrays (zeros: a valid position and row, never counted)
   std::vector<uint32_t> up((size_t)n_snps + PAD, POS_BIAS), ur((size_t)n_snps + PAD, 0u);
-  for (int i = 0; i < n_snps; i++) { up[i] = (uint32_t)pos[i] ^ POS_BIAS; ur[i] = row[i]; }
+  for (int i = 0; i < n_snps; i++) { up[i] = (uint32_t)pos[i] ^ POS_BIAS; ur[i] = row[i] + 1; }
   if ((r = upload(&c->d_pos, up.data(), up.size(), c->stream))) return r;
   if ((r = upload(&c->d_row0, ur.data(), ur.size(), c->stream))) return r;
   if ((r = upload(&c->d_row, ur.data(), ur.size(), c->stream))) return r;
@@ -822,6 +946,15 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   if ((r = upload<double>(&c->d_chr_null, nullptr, (size_t)n_chr, c->stream))) return r;
   c->n_snps = n_snps; c->n_chr = n_chr;
   c->h_chr_n.assign(chr_n, chr_n + n_chr);
+  c->h_chr_start.assign(chr_start, chr_start + n_chr);
+  c->h_pos.assign(pos, pos + n_snps);
+  c->cell_cost.clear();
+  c->h_row_cnt.clear();
+  for (int i = 0; i < n_snps; i++) {
+    if (ur[i] >= c->h_row_cnt.size()) c->h_row_cnt.resize(ur[i] + 1, 0);
+    c->h_row_cnt[ur[i]]++;
+  }
+  c->plan_dirty = true;
   return FSCLG_OK;
 }
 
@@ -829,7 +962,13 @@ int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
   if (!c || !c->d_row) return set_err(FSCLG_E_STATE, "snps not uploaded");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   if (!row) HIPCHK(hipMemcpyAsync(c->d_row, c->d_row0, sizeof(uint32_t) * c->n_snps, hipMemcpyDeviceToDevice, c->stream), "copy rows");
-  else HIPCHK(hipMemcpyAsync(c->d_row, row, sizeof(uint32_t) * c->n_snps, hipMemcpyHostToDevice, c->stream), "copy rows");
+  else {
+    c->h_stage.resize(c->n_snps);
+    for (int i = 0; i < c->n_snps; i++) c->h_stage[i] = row[i] + 1;
+    HIPCHK(hipMemcpyAsync(c->d_row, c->h_stage.data(), sizeof(uint32_t) * c->n_snps, hipMemcpyHostToDevice, c->stream),
+           "copy rows");
+    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");  // h_stage is reused
+  }
   return FSCLG_OK;
 }
 
@@ -850,6 +989,10 @@ int fsclg_set_alpha_grid(fsclg_ctx* c, const double* coarse, int n_coarse, const
   if ((r = upload(&c->d_la_refine, refine, (size_t)(n_coarse + 1) * MAXREF, c->stream))) return r;
   if ((r = upload(&c->d_n_refine, n_refine, (size_t)(n_coarse + 1), c->stream))) return r;
   c->n_coarse = n_coarse;
+  c->h_coarse.assign(coarse, coarse + n_coarse);
+  c->h_refine.assign(refine, refine + (size_t)(n_coarse + 1) * MAXREF);
+  c->h_nref.assign(n_refine, n_refine + n_coarse + 1);
+  c->plan_dirty = true;
   return FSCLG_OK;
 }
 
@@ -865,14 +1008,85 @@ static int ensure_io(fsclg_ctx* c, int n) {
   return FSCLG_OK;
 }
 
+// Choose the LDS coefficient window: intervals [ivc0, ivc0 + K) x device rows [0, R) with
+// K * R * 32 bytes beside the static LDS, thresholds and null rows in LDS_WG, maximising
+// the expected share of terms it serves = (share of sites in rows < R) x (share of terms
+// in the interval window).  The interval shares come from walks sampled on the host:
+// 32 sweep positions spread over the sites, every coarse alpha and the refine grid of the
+// first one, every 8th site of each walk, with the device's own log distance.
+static void plan_cache(fsclg_ctx* c) {
+  c->plan_dirty = false;
+  c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
+  const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
+  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8;
+  if (room < 32 || c->n_iv <= 0 || c->h_pos.empty() || c->h_coarse.empty() || c->h_lt3.empty()) return;
+  std::vector<double> hist(c->n_iv, 0.0);
+  std::vector<double> las(c->h_coarse);
+  for (int k = 0; k < c->h_nref[0]; k++) las.push_back(c->h_refine[k]);
+  const double inv = 1.0 / c->step;
+  const int S = 32, ST = 8;
+  for (int sidx = 0; sidx < S; sidx++) {
+    const int i0 = (int)(((long long)sidx * 2 + 1) * c->n_snps / (2 * S));
+    int ch = 0;
+    while (ch + 1 < c->n_chr && c->h_chr_start[ch + 1] <= i0) ch++;
+    const int a = c->h_chr_start[ch], e = a + c->h_chr_n[ch];
+    const long long sweep = (long long)c->h_pos[i0] + 1;
+    for (double la : las) {
+      for (int dir = -1; dir <= 1; dir += 2)
+        for (int i = dir < 0 ? i0 : i0 + 1; i >= a && i < e; i += dir * ST) {
+          const unsigned long long ad = (unsigned long long)llabs((long long)c->h_pos[i] - sweep);
+          const unsigned sh = ad > 0xFFFFFFull ? 16u : (ad > 0xFFFFull ? 8u : 0u);
+          const double x = c->h_lt3[(ad >> sh) + ((size_t)sh << 13)] + la;
+          if (x > LOG_AD_MAX) break;
+          int iv = (int)((x - LOG_AD_MIN) * inv);
+          iv = iv < 0 ? 0 : (iv >= c->n_iv ? c->n_iv - 1 : iv);
+          hist[iv] += 1.0;
+        }
+    }
+  }
+  double htot = 0.0;
+  for (double h : hist) htot += h;
+  long long rtot = 0;
+  for (long long n : c->h_row_cnt) rtot += n;
+  if (htot <= 0 || rtot <= 0) return;
+  std::vector<double> hpre(c->n_iv + 1, 0.0);
+  for (int j = 0; j < c->n_iv; j++) hpre[j + 1] = hpre[j] + hist[j];
+  // every row: a miss sends the whole wave's gather to the global table, so a row prefix
+  // (a per-lane miss rate) would miss in nearly every wave, while an interval window
+  // misses in whole waves (neighbouring sites have nearly equal log distance)
+  const int nrow = c->n_rows + 1;
+  long long rcum = rtot;
+  for (int R = nrow; R <= nrow; R++) {
+    const int K = std::min(c->n_iv, room / (R * 32));
+    if (K <= 0) break;
+    int bj = 0;
+    for (int j = 0; j + K <= c->n_iv; j++) if (hpre[j + K] - hpre[j] > hpre[bj + K] - hpre[bj]) bj = j;
+    const double cover = ((double)rcum / rtot) * ((hpre[bj + K] - hpre[bj]) / htot);
+    if (cover > c->c_cover) { c->c_cover = cover; c->c_ivc0 = bj; c->c_civ = K; c->c_crow = R; }
+  }
+}
+
 static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
   Params P;
   P.upos = c->d_pos; P.row = c->d_row; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
   P.thr = c->d_thr; P.n_rows = c->n_rows; P.stride = c->n_rows + 1;
   P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step;
+  // dynamic LDS: the planned coefficient window, thresholds and null rows
+  if (c->plan_dirty) plan_cache(c);
+  P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; P.n_crow = c->c_crow;
+  P.n_cache = P.n_civ * P.n_crow;
+  P.off_b = P.n_cache * 16; P.off_thr = 2 * P.off_b; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
-  P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats;
+  P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats; P.ctrace = nullptr;
+  if (getenv("FSCLG_CELL_TRACE")) {
+    if (c->ctrace_cap < n) {
+      if (c->d_ctrace) hipFree(c->d_ctrace);
+      c->d_ctrace = nullptr;
+      if (hipMalloc((void**)&c->d_ctrace, sizeof(unsigned long long) * 4 * n) == hipSuccess) c->ctrace_cap = n;
+    }
+    P.ctrace = c->d_ctrace;
+  }
   P.n_coarse = c->n_coarse; P.n_iv = c->n_iv; P.step = c->step;
   P.eval_range = eval_range; P.bp_resl = bp_resl; P.n_cells = n; P.mode = mode;
   return P;
@@ -881,9 +1095,17 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
 static int launch(fsclg_ctx* c, const Params& P, int n) {
   HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
   const int grid = (n + 7) / 8 * 8;
-  if (c->n_iv <= MAXIV && c->n_rows + 1 <= MAXROWS)
-    hipLaunchKernelGGL(search_maxpos_kernel<true>, dim3(grid), dim3(WG), 0, c->stream, P);
-  else
+  const int dyn = P.off_nul + (P.n_rows + 1) * 8;
+  const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
+  if (stat + dyn <= LDS_WG) {
+    static bool attr = false;
+    if (!attr) {
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
+      attr = true;
+    }
+    hipLaunchKernelGGL(search_maxpos_kernel<true>, dim3(grid), dim3(WG), dyn, c->stream, P);
+  } else
     hipLaunchKernelGGL(search_maxpos_kernel<false>, dim3(grid), dim3(WG), 0, c->stream, P);
   HIPCHK(hipGetLastError(), "launch search_maxpos_kernel");
   HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
@@ -907,15 +1129,54 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
   if ((r = ensure_io(c, n_cells))) return r;
-  HIPCHK(hipMemcpyAsync(c->d_cells, cells, sizeof(fsclg_cell_t) * n_cells, hipMemcpyHostToDevice, c->stream), "copy cells");
+  // longest first: each cell's cost in its last launch (permutation trials repeat the cells),
+  // else a guess (cells nearer the middle of a chromosome walk further on both sides)
+  auto key = [](const fsclg_cell_t& x) {
+    return ((unsigned long long)(uint32_t)x.chr << 58) ^ ((unsigned long long)(uint32_t)x.start_pos << 29) ^
+           (unsigned long long)(uint32_t)x.end_pos;
+  };
+  std::vector<double> cost(n_cells);
+  for (int i = 0; i < n_cells; i++) {
+    auto it = c->cell_cost.find(key(cells[i]));
+    if (it != c->cell_cost.end()) { cost[i] = it->second; continue; }
+    const int a = c->h_chr_start[cells[i].chr], nn = c->h_chr_n[cells[i].chr];
+    const double lo = c->h_pos[a], hi = c->h_pos[a + nn - 1], span = hi > lo ? hi - lo : 1.0;
+    const double m = std::min(std::max(cells[i].start_pos - lo, 0.0), std::max(hi - cells[i].start_pos, 0.0));
+    cost[i] = 1e-3 * nn * (1.0 + 2.0 * m / span);
+  }
+  c->h_order.resize(n_cells);
+  for (int i = 0; i < n_cells; i++) c->h_order[i] = i;
+  std::stable_sort(c->h_order.begin(), c->h_order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+  c->h_cells.resize(n_cells);
+  for (int k = 0; k < n_cells; k++) c->h_cells[k] = cells[c->h_order[k]];
+  HIPCHK(hipMemcpyAsync(c->d_cells, c->h_cells.data(), sizeof(fsclg_cell_t) * n_cells, hipMemcpyHostToDevice, c->stream),
+         "copy cells");
   Params P = make_params(c, n_cells, 0, eval_range, bp_resl);
   if ((r = launch(c, P, n_cells))) return r;
-  HIPCHK(hipMemcpyAsync(out, c->d_out, sizeof(fsclg_point_t) * n_cells, hipMemcpyDeviceToHost, c->stream), "copy out");
+  if (P.ctrace) {  // development aid: append [n, then n x (start, end, cu, terms)] to the file
+    std::vector<unsigned long long> h((size_t)4 * n_cells);
+    HIPCHK(hipMemcpyAsync(h.data(), P.ctrace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream),
+           "copy trace");
+    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    if (FILE* f = fopen(getenv("FSCLG_CELL_TRACE"), "ab")) {
+      const unsigned long long nn = (unsigned long long)n_cells;
+      fwrite(&nn, sizeof nn, 1, f);
+      fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+      fclose(f);
+    }
+  }
+  c->h_out.resize(n_cells);
+  HIPCHK(hipMemcpyAsync(c->h_out.data(), c->d_out, sizeof(fsclg_point_t) * n_cells, hipMemcpyDeviceToHost, c->stream),
+         "copy out");
   HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
   c->kernel_ms += ms;
   c->launches++;
+  for (int k = 0; k < n_cells; k++) {
+    out[c->h_order[k]] = c->h_out[k];
+    c->cell_cost[key(c->h_cells[k])] = c->h_out[k].cost;
+  }
   for (int i = 0; i < n_cells; i++)
     if (out[i].flags) return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL, "device flag");
   return FSCLG_OK;
@@ -963,6 +1224,8 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
   st->n_terms = h[0]; st->n_null = h[1]; st->n_walks = h[2]; st->n_maxalpha = h[3];
   st->n_unsafe = h[4]; st->n_slow = h[5]; st->n_ties = h[6]; st->n_cells = h[7];
   st->kernel_ms = c->kernel_ms; st->n_launches = c->launches;
+  if (c->plan_dirty) plan_cache(c);
+  st->cache_iv0 = c->c_ivc0; st->cache_n_iv = c->c_civ; st->cache_n_rows = c->c_crow; st->cache_cover = c->c_cover;
   return FSCLG_OK;
 }
 

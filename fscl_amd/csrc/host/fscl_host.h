@@ -24,17 +24,24 @@ int fh_rand(fh_rand_t *g);
 double fh_log_fact(int n);
 void fh_log_fact_reserve(int n);
 
-/* spline row layout: per depth, (n+1) unfolded then (n/2+1) folded rows */
+/* spline row layout: per depth, (n+1) unfolded then (n/2+1) folded rows; the device holds
+   only the rows some site uses, renumbered in that order */
 typedef struct {
   int n_depths;
   int *depth_n;      /* sample size of each depth index */
   int *row_base;     /* first row of each depth */
-  int n_rows;
+  int n_rows;        /* all rows */
   int n_iv;          /* spline intervals (spline_pts) */
+  int *dev_row;      /* [n_rows] device row of each row, -1 if no site uses it */
+  int n_dev_rows;
 } fh_rowmap_t;
 
-static inline uint32_t fh_row_of(const fh_rowmap_t *m, const snp_t *s) {
+static inline uint32_t fh_full_row(const fh_rowmap_t *m, const snp_t *s) {
   return (uint32_t)(m->row_base[s->depth_p] + (s->folded ? m->depth_n[s->depth_p] + 1 + s->obs_freq : s->obs_freq));
+}
+
+static inline uint32_t fh_row_of(const fh_rowmap_t *m, const snp_t *s) {
+  return (uint32_t)m->dev_row[fh_full_row(m, s)];
 }
 
 /* current global log_ad_step (sm-spline.c:16,325) */

@@ -145,7 +145,7 @@ static void dev_check(int r, const char *what) {
 }
 
 static void free_rowmap(fh_rowmap_t *m) {
-  free(m->depth_n); free(m->row_base);
+  free(m->depth_n); free(m->row_base); free(m->dev_row);
   memset(m, 0, sizeof *m);
 }
 
@@ -170,29 +170,58 @@ static void upload_tables(const sm_ptable_t *sm, int n_depths, const int *depth_
     m->n_rows += depth_n[d] + 1 + depth_n[d] / 2 + 1;
   }
   m->n_iv = sm[0].spline_func[0]->n;
-  coef = fh_malloc(sizeof(double) * (size_t)m->n_rows * m->n_iv * 4, "flat tables");
+  /* null_logl is a function of the row (scan-chromosome.c:23-37): take it from the sites;
+     the rows no site uses are dropped from the device tables */
+  seen = fh_calloc(m->n_rows, 1, "null rows");
+  m->dev_row = fh_malloc(sizeof(int) * m->n_rows, "rowmap");
+  {
+    double *full_null = fh_calloc(m->n_rows, sizeof(double), "null rows");
+    for (i = 0; i < n_idx; i++) {
+      const snp_t *p = snps + (idx ? idx[i] : i);
+      const uint32_t rr = fh_full_row(m, p);
+      if (!seen[rr]) { full_null[rr] = p->null_logl; seen[rr] = 1; }
+      else if (memcmp(&full_null[rr], &p->null_logl, sizeof(double)) != 0)
+        logmsg(MSG_FATAL, "fscl_amd: null_logl differs between sites of the same class (call "
+                          "compute_snp_null_model first)");
+    }
+    /* device rows in descending order of site count (ties by row): the device caches a
+       prefix of them in LDS */
+    {
+      long long *cnt = fh_calloc(m->n_rows, sizeof(long long), "row counts");
+      int *ord = fh_malloc(sizeof(int) * m->n_rows, "row order");
+      int nu = 0, a, b;
+      for (i = 0; i < n_idx; i++) cnt[fh_full_row(m, snps + (idx ? idx[i] : i))]++;
+      for (r = 0; r < m->n_rows; r++) if (seen[r]) ord[nu++] = r;
+      for (a = 1; a < nu; a++) {  /* insertion sort: a few hundred rows */
+        const int v = ord[a];
+        for (b = a; b > 0 && (cnt[ord[b - 1]] < cnt[v] || (cnt[ord[b - 1]] == cnt[v] && ord[b - 1] > v)); b--)
+          ord[b] = ord[b - 1];
+        ord[b] = v;
+      }
+      for (r = 0; r < m->n_rows; r++) m->dev_row[r] = -1;
+      for (a = 0; a < nu; a++) m->dev_row[ord[a]] = a;
+      m->n_dev_rows = nu;
+      free(cnt);
+      free(ord);
+    }
+    if (m->n_dev_rows == 0) m->n_dev_rows = 1;  /* no sites: one zero row keeps the tables well-formed */
+    nullrow = fh_calloc(m->n_dev_rows, sizeof(double), "null rows");
+    for (r = 0; r < m->n_rows; r++) if (seen[r]) nullrow[m->dev_row[r]] = full_null[r];
+    free(full_null);
+  }
+  coef = fh_calloc((size_t)m->n_dev_rows * m->n_iv * 4, sizeof(double), "flat tables");
   for (d = 0; d < n_depths; d++) {
     const int n = depth_n[d];
     for (r = 0; r <= n + n / 2 + 1; r++) {
       const spline_t *sp = r <= n ? sm[d].spline_func[r] : sm[d].fspline_func[r - n - 1];
-      double *dst = coef + (size_t)(m->row_base[d] + r) * m->n_iv * 4;
+      const int dr = m->dev_row[m->row_base[d] + r];
       if (sp->n != m->n_iv) logmsg(MSG_FATAL, "fscl_amd: splines with different knot counts");
-      for (i = 0; i < sp->n; i++) memcpy(dst + 4 * i, sp->coef[i], sizeof(double) * 4);
+      if (dr < 0) continue;
+      for (i = 0; i < sp->n; i++) memcpy(coef + ((size_t)dr * m->n_iv + i) * 4, sp->coef[i], sizeof(double) * 4);
     }
   }
-  /* null_logl is a function of the row (scan-chromosome.c:23-37): take it from the sites */
-  nullrow = fh_calloc(m->n_rows, sizeof(double), "null rows");
-  seen = fh_calloc(m->n_rows, 1, "null rows");
-  for (i = 0; i < n_idx; i++) {
-    const snp_t *p = snps + (idx ? idx[i] : i);
-    const uint32_t rr = fh_row_of(m, p);
-    if (!seen[rr]) { nullrow[rr] = p->null_logl; seen[rr] = 1; }
-    else if (memcmp(&nullrow[rr], &p->null_logl, sizeof(double)) != 0)
-      logmsg(MSG_FATAL, "fscl_amd: null_logl differs between sites of the same class (call "
-                        "compute_snp_null_model first)");
-  }
   /* log_ad_step of the tables' knot grid (sm-spline.c:325) */
-  dev_check(fsclg_upload_tables(D.ctx, fh_log_table(), coef, m->n_rows, m->n_iv, nullrow,
+  dev_check(fsclg_upload_tables(D.ctx, fh_log_table(), coef, m->n_dev_rows, m->n_iv, nullrow,
                                 (LOG_AD_MAX - LOG_AD_MIN) / (m->n_iv + 1.)),
             "upload tables");
   free(D.nullrow);
@@ -625,6 +654,8 @@ void fscl_amd_get_stats(fscl_amd_stats_t *st) {
       st->kernel_ms = g.kernel_ms;
       st->n_terms = g.n_terms; st->n_null = g.n_null; st->n_walks = g.n_walks; st->n_maxalpha = g.n_maxalpha;
       st->n_unsafe = g.n_unsafe; st->n_slow = g.n_slow; st->n_ties = g.n_ties; st->n_launches = g.n_launches;
+      st->cache_iv0 = g.cache_iv0; st->cache_n_iv = g.cache_n_iv; st->cache_n_rows = g.cache_n_rows;
+      st->cache_cover = g.cache_cover;
     }
   }
 }

@@ -166,6 +166,8 @@ typedef struct {
   unsigned long long n_terms, n_null, n_walks, n_maxalpha, n_unsafe, n_slow, n_ties, n_launches;
   unsigned long long negj; /* permutation blocks that hit the reference's negative-j bug (repaired) */
   int trials;             /* permutation trials run */
+  int cache_iv0, cache_n_iv, cache_n_rows;  /* LDS coefficient window (fsclg_stats_t) */
+  double cache_cover;
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

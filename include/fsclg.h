@@ -46,7 +46,8 @@ typedef struct {
 
 /* one evaluated scan point (the fields of scan_pt_t the path produces) */
 typedef struct {
-  int32_t chr, nearest_snp, sweep_pos, n_snps, window_start, window_end, flags, pad;
+  int32_t chr, nearest_snp, sweep_pos, n_snps, window_start, window_end, flags;
+  uint32_t cost;  /* out: snp_likelihood terms / 1024 spent on this point's cell (scheduling hint) */
   double lalpha, null_logl, sm_logl, clr;
 } fsclg_point_t;
 
@@ -62,6 +63,8 @@ typedef struct {
   unsigned long long n_cells;      /* search_maxpos evaluations */
   double kernel_ms;                /* summed duration of the search kernels (HIP events) */
   unsigned long long n_launches;
+  int cache_iv0, cache_n_iv, cache_n_rows;  /* LDS coefficient window: intervals, device rows */
+  double cache_cover;              /* its planned share of the terms */
 } fsclg_stats_t;
 
 int fsclg_open(int device, fsclg_ctx **out);
