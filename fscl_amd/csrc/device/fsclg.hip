@@ -70,8 +70,7 @@ constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsi
 enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2 };
 
 struct Params {
-  const uint32_t* upos;        // [n_snps + PAD] position ^ POS_BIAS
-  const uint32_t* row;         // [n_snps + PAD] device row = caller's row + 1 (0: the zero sentinel)
+  const uint2* pr;             // [n_snps + PAD] (position ^ POS_BIAS, device row = caller's row + 1; 0: zero sentinel)
   const double* logt3;         // [3][65536]: c_b + log_table[i], the three branches of sm-search.c:40-46
   const double* coef;          // [n_iv][n_rows + 1][4], device row 0 all zero (sentinel)
   const double* nullrow;       // [n_rows + 1], entry 0 zero
@@ -92,10 +91,10 @@ struct Params {
   int stride;                  // n_rows + 1
   double step;
   double inv_step;
-  double iv_off;               // -LOG_AD_MIN * inv_step
-  int ivc0;                    // LDS coefficient cache: intervals [ivc0, ivc0 + n_civ) x device rows [0, n_crow)
-  int n_civ, n_crow;
-  int n_cache;                 // n_civ * n_crow blocks
+  double iv_off;               // -LOG_AD_MIN * inv_step - 1e-9 (interval_of)
+  int ivc0;                    // LDS coefficient cache: intervals [ivc0, ivc0 + n_civ), every row
+  int n_civ, civ_max;          // civ_max = max(n_civ - 1, 0)
+  int n_cache;                 // n_civ * stride blocks
   int off_b, off_thr, off_nul; // byte offsets in fsclg_dyn (plane A at 0)
   int eval_range;
   int bp_resl;
@@ -142,12 +141,11 @@ struct Smem {
 // interval thresholds and the null rows (offsets in Params)
 extern __shared__ __attribute__((aligned(16))) char fsclg_dyn[];
 
-__device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t i) {
-  // 32-bit byte offset from a scalar base (global_load saddr + voffset)
-  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(base) + (i << 2));
+__device__ __forceinline__ uint2 ld_pr(const uint2* base, uint32_t i) {
+  return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(base) + (i << 3));
 }
 
-__device__ __forceinline__ int pos_at(const Params& P, int i) { return (int)(P.upos[i] ^ POS_BIAS); }
+__device__ __forceinline__ int pos_at(const Params& P, int i) { return (int)(P.pr[i].x ^ POS_BIAS); }
 
 // log of |d| as sm-search.c:40-46: three branches, each c_b + log_table[|d| >> 8b], merged
 // into one precomputed table (the host forms c_b + log_table[i] with the same IEEE add)
@@ -165,23 +163,21 @@ __device__ __forceinline__ uint32_t absdist(uint32_t upos, uint32_t usweep) {
 }
 
 __device__ __forceinline__ double log_ad_of(int i, int sweep, double la, const Params& P) {
-  return logt_dev(absdist(P.upos[i], (uint32_t)sweep ^ POS_BIAS), P.logt3) + la;
+  return logt_dev(absdist(P.pr[i].x, (uint32_t)sweep ^ POS_BIAS), P.logt3) + la;
 }
 
 // spline interval of sm-spline.c:52-54, (int)((x - LOG_AD_MIN) / step) clamped, without the
-// division: an fma estimate is within one of it, and exact thresholds settle it
-// (thr[0] = -inf and thr[n_iv] = +inf make the correction branch-free)
+// division: an fma estimate lowered by 1e-9 (its error and the reference's rounding are
+// ~1e-13) is the interval or the one below it, and the exact threshold of the next one
+// settles it (thr[n_iv] = +inf: the reference clamps at n_iv - 1)
 template <bool LDS>
 __device__ __forceinline__ int interval_of(double x, const Smem& S, const Params& P) {
   int iv = (int)__builtin_fma(x, P.inv_step, P.iv_off);
   iv = min(max(iv, 0), P.n_iv - 1);
-  double lo, hi;
-  if constexpr (LDS) {
-    const double* t = reinterpret_cast<const double*>(fsclg_dyn + P.off_thr);
-    lo = t[iv]; hi = t[iv + 1];
-  }
-  else { lo = P.thr[iv]; hi = P.thr[iv + 1]; }
-  return iv + (x >= hi ? 1 : 0) - (x < lo ? 1 : 0);
+  double hi;
+  if constexpr (LDS) hi = reinterpret_cast<const double*>(fsclg_dyn + P.off_thr)[iv + 1];
+  else hi = P.thr[iv + 1];
+  return iv + (x >= hi ? 1 : 0);
 }
 
 template <bool LDS>
@@ -209,8 +205,8 @@ __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Params& P, 
   if constexpr (LDS) {
 #endif
     const uint32_t ci = (uint32_t)(iv - P.ivc0);
-    const bool hit = ci < (uint32_t)P.n_civ && r < (uint32_t)P.n_crow;
-    const uint32_t li = __umul24(min(ci, (uint32_t)P.n_civ - 1), (uint32_t)P.n_crow) + min(r, (uint32_t)P.n_crow - 1);
+    const bool hit = ci < (uint32_t)P.n_civ;  // every row is cached
+    const uint32_t li = __umul24(min(ci, (uint32_t)P.civ_max), (uint32_t)P.stride) + r;
     a = reinterpret_cast<const double2*>(fsclg_dyn)[li];
     b = reinterpret_cast<const double2*>(fsclg_dyn + P.off_b)[li];
     if (!hit) {
@@ -225,9 +221,8 @@ __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Params& P, 
   }
 }
 
-// coefficients of U terms, in stages so the loads of all U overlap: interval estimates and
-// their threshold reads, the corrections, the LDS reads, then one wave-uniform branch that
-// gathers the misses from the global table into separate registers and selects them
+// coefficients of U terms: the intervals of all U first (their threshold reads overlap),
+// then per term the LDS window or, for lanes outside it, the global table
 template <bool LDS>
 __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t (&rv)[U], const Smem& S,
                                            const Params& P, double2 (&ca)[U], double2 (&cb)[U]) {
@@ -240,31 +235,17 @@ __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t 
 #pragma unroll
   for (int u = 0; u < U; u++) iv[u] = interval_of<LDS>(x[u], S, P);
   if constexpr (CACHE) {
-    bool hit[U];
-    bool miss = false;
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t ci = (uint32_t)(iv[u] - P.ivc0);
-      hit[u] = ci < (uint32_t)P.n_civ && rv[u] < (uint32_t)P.n_crow;
-      miss |= !hit[u];
-      const uint32_t li = __umul24(min(ci, (uint32_t)P.n_civ - 1), (uint32_t)P.n_crow) + min(rv[u], (uint32_t)P.n_crow - 1);
-      ca[u] = reinterpret_cast<const double2*>(fsclg_dyn)[li];
-      cb[u] = reinterpret_cast<const double2*>(fsclg_dyn + P.off_b)[li];
-    }
-    if (__ballot(miss)) {
-      double2 ga[U], gb[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
+      if (ci < (uint32_t)P.n_civ) {  // every row is cached
+        const uint32_t li = __umul24(ci, (uint32_t)P.stride) + rv[u];
+        ca[u] = reinterpret_cast<const double2*>(fsclg_dyn)[li];
+        cb[u] = reinterpret_cast<const double2*>(fsclg_dyn + P.off_b)[li];
+      } else {
         const double2* cp = coef_of(rv[u], iv[u], P);
-        ga[u] = cp[0];
-        gb[u] = cp[1];
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {  // component selects (a double2 ternary becomes a stack-address select)
-        ca[u].x = hit[u] ? ca[u].x : ga[u].x;
-        ca[u].y = hit[u] ? ca[u].y : ga[u].y;
-        cb[u].x = hit[u] ? cb[u].x : gb[u].x;
-        cb[u].y = hit[u] ? cb[u].y : gb[u].y;
+        ca[u] = cp[0];
+        cb[u] = cp[1];
       }
     }
   } else {
@@ -282,7 +263,7 @@ template <bool LDS>
 __device__ __forceinline__ double term_dev(int i, int sweep, double la, const Smem& S, const Params& P) {
   const double x = log_ad_of(i, sweep, la, P);
   const int iv = interval_of<LDS>(x, S, P);
-  const uint32_t r = P.row[i];
+  const uint32_t r = P.pr[i].y;
   double2 a, b;
   coef_fetch<LDS>(r, iv, P, a, b);
   const double y = x * (a.x * x * x + a.y * x + b.x) + b.y;
@@ -401,9 +382,11 @@ __device__ __forceinline__ void seg_range(const Walk& W, int s, int& jb, int& je
 // one segment (<= 1024 terms) of one walk, by one wave, in index order: U terms per
 // lane per trip with all loads issued first; lanes past the segment read the padding
 // and take the zero sentinel row (term exactly 0).  Per lane: R = rint(t/u) summed in
-// fp64 (exact: < 2^53, checked once per segment) together with sum |R|.
+// fp64 into the wave's accumulators for this walk (acc = sum R, accm = sum |R|; exact
+// while accm < 2^51, checked when the wave flushes the walk); the segment's parity bit
+// (for the tie replay) from one ballot.
 template <bool LDS>
-__device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane) {
+__device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane, double& acc, double& accm) {
 #ifdef FSCLG_EXP_NOTERMS  // timing ablation only: skip every term
   return;
 #endif
@@ -420,8 +403,9 @@ __device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t i = lo + (uint32_t)(kb + 64 * u + lane);
-      pv[u] = ld_u32(P.upos, i);
-      rv[u] = ld_u32(P.row, i);
+      const uint2 v = ld_pr(P.pr, i);
+      pv[u] = v.x;
+      rv[u] = v.y;
     }
 #pragma unroll
     for (int u = 0; u < U; u++)
@@ -451,17 +435,25 @@ __device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane) {
       mag += fabs(R);
     }
   }
-  // exactness: every partial of |R| below 2^53 (fl is monotone, so fl(mag) < 2^53 says so,
-  // NaN fails it), and the walk's int64 totals below 2^61
-  const double limA = fmin(9007199254740992.0, 36028797018963968.0 / (double)W.nseg);  // 2^53, 2^55/nseg
-  const bool big = !(mag < limA);
-  const long long isum = wave_sum64((long long)sum);
-  const long long imag = wave_sum64((long long)mag);
+  // the segment's parity: sum over lanes of (sum mod 2); partials are exact integers
+  // whenever the walk passes its flush check (otherwise its value is discarded)
+  const unsigned long long odd = __ballot(sum - 2.0 * floor(0.5 * sum) != 0.0);
+  if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
+  acc += sum;
+  accm += mag;
+}
+
+// a wave's share of walk w: int64 totals of sum R and sum |R| into S.P / S.Q.  Exact when
+// every lane's |R| total is below 2^51 (then all fp64 partials were exact, fl being
+// monotone; NaN fails the test); 8 waves x 64 lanes keep the walk's totals below 2^60.
+__device__ void flush_walk(Smem& S, int w, double acc, double accm, int lane) {
+  const bool big = !(accm < 2251799813685248.0);  // 2^51
+  const long long isum = wave_sum64(big ? 0 : (long long)acc);
+  const long long imag = wave_sum64(big ? 0 : (long long)accm);
   const bool anybig = __any(big);
   if (lane == 0) {
     atomicAdd(&S.P[w], (unsigned long long)isum);
     atomicAdd(&S.Q[w], (unsigned long long)imag);
-    if (isum & 1) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
     if (anybig) atomicOr(&S.wflag[w], 1);
   }
 }
@@ -564,11 +556,17 @@ __device__ void eval_walks(Smem& S, const Params& P) {
   // miscompiled into a loop that never re-issued its atomic)
   {
     const int total = __builtin_amdgcn_readfirstlane(S.seg_total);
-    int w = 0;
+    int w = 0, cw = -1;
+    double acc = 0.0, accm = 0.0;
     for (int g = wave; g < total; g += NWAVE) {
       while (w < nw - 1 && g >= S.w[w].seg0 + S.w[w].nseg) w++;  // walks own consecutive segment ranges
-      run_segment<LDS>(S, w, g - S.w[w].seg0, P, lane);
+      if (w != cw) {  // the wave's segments of one walk are consecutive: flush once per walk
+        if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
+        cw = w; acc = 0.0; accm = 0.0;
+      }
+      run_segment<LDS>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
     }
+    if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
   }
   __syncthreads();
   TRACE("  segments done: ties=%d\n", S.n_ties);
@@ -701,7 +699,7 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
     for (int j = tid; j <= P.n_rows; j += WG) nul[j] = P.nullrow[j];  // + sentinel
     // planes [ci][row] of the cached window
     for (int e = tid; e < P.n_cache; e += WG) {
-      const int ci = e / P.n_crow, r = e - ci * P.n_crow;
+      const int ci = e / P.stride, r = e - ci * P.stride;
       const double2* src = reinterpret_cast<const double2*>(P.coef) + ((size_t)(P.ivc0 + ci) * P.stride + r) * 2;
       ca[e] = src[0];
       cb[e] = src[1];
@@ -771,9 +769,9 @@ struct fsclg_ctx {
   int n_rows = 0, n_iv = 0;
   double step = 0.0;
   // snps
-  uint32_t* d_pos = nullptr;      // biased positions, n_snps + PAD
-  uint32_t* d_row0 = nullptr;
-  uint32_t* d_row = nullptr;
+  uint2* d_pr = nullptr;          // (biased position, device row), n_snps + PAD
+  uint2* d_pr0 = nullptr;         // the same with the unpermuted rows
+  std::vector<uint2> h_pr0;
   int n_snps = 0;
   int32_t* d_chr_start = nullptr;
   int32_t* d_chr_n = nullptr;
@@ -783,7 +781,7 @@ struct fsclg_ctx {
   std::vector<int32_t> h_pos, h_chr_start;
   std::vector<long long> h_row_cnt;     // sites per device row
   std::vector<double> h_lt3;
-  std::vector<uint32_t> h_stage;
+  std::vector<uint2> h_stage;
   // LDS coefficient cache plan (fsclg_plan_cache)
   bool plan_dirty = true;
   int c_ivc0 = 0, c_civ = 0, c_crow = 0;
@@ -878,7 +876,7 @@ int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_ctrace, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pos, c->d_row0, c->d_row, c->d_chr_start, c->d_chr_n,
+  void* ptrs[] = {c->d_ctrace, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr, c->d_pr0, c->d_chr_start, c->d_chr_n,
                   c->d_chr_null, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   hipEventDestroy(c->ev0);
@@ -936,11 +934,10 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
   // PAD slack after both arrays (zeros: a valid position and row, never counted)
-  std::vector<uint32_t> up((size_t)n_snps + PAD, POS_BIAS), ur((size_t)n_snps + PAD, 0u);
-  for (int i = 0; i < n_snps; i++) { up[i] = (uint32_t)pos[i] ^ POS_BIAS; ur[i] = row[i] + 1; }
-  if ((r = upload(&c->d_pos, up.data(), up.size(), c->stream))) return r;
-  if ((r = upload(&c->d_row0, ur.data(), ur.size(), c->stream))) return r;
-  if ((r = upload(&c->d_row, ur.data(), ur.size(), c->stream))) return r;
+  std::vector<uint2> pr((size_t)n_snps + PAD, make_uint2(POS_BIAS, 0u));
+  for (int i = 0; i < n_snps; i++) pr[i] = make_uint2((uint32_t)pos[i] ^ POS_BIAS, row[i] + 1);
+  if ((r = upload(&c->d_pr0, pr.data(), pr.size(), c->stream))) return r;
+  if ((r = upload(&c->d_pr, pr.data(), pr.size(), c->stream))) return r;
   if ((r = upload(&c->d_chr_start, chr_start, (size_t)n_chr, c->stream))) return r;
   if ((r = upload(&c->d_chr_n, chr_n, (size_t)n_chr, c->stream))) return r;
   if ((r = upload<double>(&c->d_chr_null, nullptr, (size_t)n_chr, c->stream))) return r;
@@ -951,21 +948,25 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   c->cell_cost.clear();
   c->h_row_cnt.clear();
   for (int i = 0; i < n_snps; i++) {
-    if (ur[i] >= c->h_row_cnt.size()) c->h_row_cnt.resize(ur[i] + 1, 0);
-    c->h_row_cnt[ur[i]]++;
+    if (pr[i].y >= c->h_row_cnt.size()) c->h_row_cnt.resize(pr[i].y + 1, 0);
+    c->h_row_cnt[pr[i].y]++;
   }
+  c->h_pr0.swap(pr);
   c->plan_dirty = true;
   return FSCLG_OK;
 }
 
 int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
-  if (!c || !c->d_row) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  if (!c || !c->d_pr) return set_err(FSCLG_E_STATE, "snps not uploaded");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
-  if (!row) HIPCHK(hipMemcpyAsync(c->d_row, c->d_row0, sizeof(uint32_t) * c->n_snps, hipMemcpyDeviceToDevice, c->stream), "copy rows");
+  if (!row) HIPCHK(hipMemcpyAsync(c->d_pr, c->d_pr0, sizeof(uint2) * c->n_snps, hipMemcpyDeviceToDevice, c->stream), "copy rows");
   else {
     c->h_stage.resize(c->n_snps);
-    for (int i = 0; i < c->n_snps; i++) c->h_stage[i] = row[i] + 1;
-    HIPCHK(hipMemcpyAsync(c->d_row, c->h_stage.data(), sizeof(uint32_t) * c->n_snps, hipMemcpyHostToDevice, c->stream),
+    for (int i = 0; i < c->n_snps; i++) {
+      if (row[i] >= (uint32_t)c->n_rows) return set_err(FSCLG_E_ARG, "row index out of table");
+      c->h_stage[i] = make_uint2(c->h_pr0[i].x, row[i] + 1);
+    }
+    HIPCHK(hipMemcpyAsync(c->d_pr, c->h_stage.data(), sizeof(uint2) * c->n_snps, hipMemcpyHostToDevice, c->stream),
            "copy rows");
     HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");  // h_stage is reused
   }
@@ -1068,13 +1069,13 @@ static void plan_cache(fsclg_ctx* c) {
 
 static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
   Params P;
-  P.upos = c->d_pos; P.row = c->d_row; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
+  P.pr = c->d_pr; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
   P.thr = c->d_thr; P.n_rows = c->n_rows; P.stride = c->n_rows + 1;
-  P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step;
+  P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step - 1e-9;
   // dynamic LDS: the planned coefficient window, thresholds and null rows
   if (c->plan_dirty) plan_cache(c);
-  P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; P.n_crow = c->c_crow;
-  P.n_cache = P.n_civ * P.n_crow;
+  P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; P.civ_max = std::max(c->c_civ - 1, 0);
+  P.n_cache = P.n_civ * P.stride;
   P.off_b = P.n_cache * 16; P.off_thr = 2 * P.off_b; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
@@ -1115,7 +1116,7 @@ static int launch(fsclg_ctx* c, const Params& P, int n) {
 int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, int eval_range, int bp_resl,
                         fsclg_point_t* out) {
   if (!c || (!cells && n_cells) || (!out && n_cells) || n_cells < 0) return set_err(FSCLG_E_ARG, "cells");
-  if (!c->d_pos || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
+  if (!c->d_pr || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
   if (n_cells == 0) return FSCLG_OK;
   // host-side shape checks before any launch
   if (eval_range < 0 || bp_resl < 0) return set_err(FSCLG_E_ARG, "eval_range/bp_resl");
@@ -1184,7 +1185,7 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
 
 int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
   if (!c || (!pts && n_pts) || n_pts < 0) return set_err(FSCLG_E_ARG, "points");
-  if (!c->d_pos || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
+  if (!c->d_pr || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
   if (n_pts == 0) return FSCLG_OK;
   for (int i = 0; i < n_pts; i++) {
     const fsclg_point_t& p = pts[i];
