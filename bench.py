@@ -168,7 +168,7 @@ def main() -> int:
         "setup_s": setup_s,
         "stats": {k: st[k] for k in ("n_terms", "n_null", "n_walks", "n_unsafe", "n_slow", "n_ties", "trials",
                                      "host_perm_s", "scan_s", "permute_s", "gp_evals",
-                                     "cache_iv0", "cache_n_iv", "cache_n_rows", "cache_cover")},
+                                     "cache_iv0", "cache_n_iv", "cache_n_rows", "cache_cover", "window_ms")},
     }
 
     # ---- CPU baseline: the oracle port on the host cores, bounded sample = the initial scan

@@ -51,11 +51,14 @@ namespace {
 #endif
 constexpr int WG = FSCLG_WG;
 constexpr int NWAVE = WG / 64;
-constexpr int SEG = 1024;          // terms per work segment
+#ifndef FSCLG_SEG
+#define FSCLG_SEG 1024
+#endif
+constexpr int SEG = FSCLG_SEG;     // terms per work segment
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
 constexpr int MAXSEG_W = 192;      // segments per walk (161 at 163841 terms)
 constexpr int SEGWORDS = MAXSEG_W / 32;
-constexpr int MAXTIES = 2048;
+constexpr int MAXTIES = 512;       // per eval_walks; overflow sends the affected argmax to the exact slow path
 constexpr int MAXREF = 16;
 constexpr int LDS_WG = FSCLG_LDS_WG;  // LDS per workgroup (default: two workgroups per CU, 160 KiB)
 #ifndef FSCLG_U
@@ -77,7 +80,8 @@ struct Params {
   const double* thr;           // thr[j] = least x with (int)((x - LOG_AD_MIN) / step) >= j, j = 1..n_iv-1
   const int32_t* chr_start;
   const int32_t* chr_n;
-  const double* chr_null;
+  const double* chr_null;      // [n_chr] null sum of a whole chromosome (windows that are the chromosome)
+  const double* win_null;      // [n_snps] null sum of the window starting at ws (chromosomes above 2*eval_range+1 SNPs)
   const double* la_coarse;     // [n_coarse]
   const double* la_refine;     // [n_coarse + 1][MAXREF]; row n_coarse: around LOG_AD_MAX
   const int32_t* n_refine;     // [n_coarse + 1]
@@ -85,6 +89,7 @@ struct Params {
   fsclg_point_t* out;
   unsigned long long* stats;   // 8 counters
   unsigned long long* ctrace;  // optional per-cell [start, end, cu id, terms] (FSCLG_CELL_TRACE)
+  unsigned long long* ivhist;  // optional [n_iv]: terms per spline interval, one sample per segment
   int n_coarse;
   int n_iv;
   int n_rows;
@@ -307,8 +312,9 @@ __device__ void init_point(Pt& pt, int chr, int pos, const Params& P) {
   pt.chr = chr; pt.nearest = near; pt.sweep = pos; pt.wstart = ws; pt.wend = we;
   pt.n_snps = we - ws + 1;
   pt.flags = 0;
-  if (ws != cs || we != ce) pt.flags |= PF_UNSUPPORTED;
-  pt.N = P.chr_null[chr];
+  // scan-chromosome.c:92-94 (sequential sum from 0.0 over the window): the whole
+  // chromosome's per trial from the host, a proper window's from window_null_kernel
+  pt.N = (ws == cs && we == ce) ? P.chr_null[chr] : P.win_null[ws];
 }
 
 // binade constants of the start value N: |N| in [2^e, 2^(e+1)), u = 2^(e-52)
@@ -413,6 +419,8 @@ __device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane, do
     double x[U];
 #pragma unroll
     for (int u = 0; u < U; u++) x[u] = logt_dev(absdist(pv[u], usweep), P.logt3) + la;
+    if (P.ivhist && kb == jb && lane == 0)  // one sample per segment, weighted by its terms
+      atomicAdd(&P.ivhist[interval_of<LDS>(x[0], S, P)], (unsigned long long)(je - jb));
     double2 ca[U], cb[U];
     coef_stage<LDS>(x, rv, S, P, ca, cb);
 #pragma unroll
@@ -754,6 +762,58 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
   if (P.ctrace && tid == 0) { P.ctrace[4 * cell + 1] = wall_clock64(); P.ctrace[4 * cell + 3] = S.cnt[0]; }
 }
 
+// ------------------------------------------------------------ window null sums
+// init_scan_result's window sum (scan-chromosome.c:92-94) for every window start of the
+// chromosomes longer than the window: acc = 0.0; acc += null_logl[i] for i = ws..ws+W-1,
+// in that order, per window.  A thread carries WN_PER neighbouring windows (each element
+// read once from LDS feeds all of them, each accumulator in its own ascending order); the
+// block stages the elements its 1024 windows span through an LDS tile.
+constexpr int WN_WG = 256, WN_PER = 4, WN_TILE = 4096;
+
+__global__ void __launch_bounds__(WN_WG) window_null_kernel(const uint2* __restrict__ pr,
+                                                            const double* __restrict__ nullrow,
+                                                            const int2* __restrict__ tasks, int W,
+                                                            double* __restrict__ out) {
+  __shared__ double tile[WN_TILE];
+  const int2 t = tasks[blockIdx.x];  // windows [t.x, t.x + t.y)
+  const int k = threadIdx.x;
+  const int base = t.x + WN_PER * k;
+  const int nwin = min(max(t.y - WN_PER * k, 0), WN_PER);
+  const int end = t.x + t.y - 1 + W;  // one past the last element a window of the block uses
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  for (int T0 = t.x; T0 < end; T0 += WN_TILE) {
+    const int T1 = min(T0 + WN_TILE, end);
+    __syncthreads();
+    for (int j = T0 + k; j < T1; j += WN_WG) tile[j - T0] = nullrow[pr[j].y];
+    __syncthreads();
+    if (nwin == 0) continue;
+    const int lo = max(T0, base), hi = min(T1, base + nwin - 1 + W);
+    // window m takes elements base + m .. base + m + W - 1
+    auto edge = [&](int j0, int j1) {
+      for (int j = j0; j < j1; j++) {
+        const double v = tile[j - T0];
+        const int off = j - base;
+        if (off < W) a0 += v;
+        if (nwin > 1 && off >= 1 && off < W + 1) a1 += v;
+        if (nwin > 2 && off >= 2 && off < W + 2) a2 += v;
+        if (nwin > 3 && off >= 3 && off < W + 3) a3 += v;
+      }
+    };
+    if (nwin < WN_PER) { edge(lo, hi); continue; }
+    const int m0 = min(max(lo, base + WN_PER - 1), hi), m1 = max(min(hi, base + W), m0);
+    edge(lo, m0);
+    for (int j = m0; j < m1; j++) {  // every window of the thread takes these
+      const double v = tile[j - T0];
+      a0 += v; a1 += v; a2 += v; a3 += v;
+    }
+    edge(m1, hi);
+  }
+  if (nwin > 0) out[base] = a0;
+  if (nwin > 1) out[base + 1] = a1;
+  if (nwin > 2) out[base + 2] = a2;
+  if (nwin > 3) out[base + 3] = a3;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------- host shim
@@ -776,6 +836,11 @@ struct fsclg_ctx {
   int32_t* d_chr_start = nullptr;
   int32_t* d_chr_n = nullptr;
   double* d_chr_null = nullptr;
+  double* d_win_null = nullptr;           // [n_snps], valid for (win_er, rows) while win_valid
+  int2* d_wtasks = nullptr;
+  int n_wtasks = 0, wtask_cap = 0, win_er = -1;
+  bool win_valid = false;
+  double window_ms = 0.0;
   int n_chr = 0;
   std::vector<int> h_chr_n;
   std::vector<int32_t> h_pos, h_chr_start;
@@ -784,6 +849,9 @@ struct fsclg_ctx {
   std::vector<uint2> h_stage;
   // LDS coefficient cache plan (fsclg_plan_cache)
   bool plan_dirty = true;
+  bool hist_pending = false;          // the next search_maxpos launch measures the interval histogram
+  unsigned long long* d_ivhist = nullptr;
+  int ivhist_n = 0;
   int c_ivc0 = 0, c_civ = 0, c_crow = 0;
   double c_cover = 0.0;
   // alpha grid
@@ -876,8 +944,8 @@ int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_ctrace, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr, c->d_pr0, c->d_chr_start, c->d_chr_n,
-                  c->d_chr_null, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
+  void* ptrs[] = {c->d_ctrace, c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr, c->d_pr0, c->d_chr_start, c->d_chr_n,
+                  c->d_chr_null, c->d_win_null, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   hipEventDestroy(c->ev0);
   hipEventDestroy(c->ev1);
@@ -921,6 +989,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->stream))) return r;
   c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
   c->plan_dirty = true;
+  c->win_valid = false;
   return FSCLG_OK;
 }
 
@@ -941,6 +1010,8 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   if ((r = upload(&c->d_chr_start, chr_start, (size_t)n_chr, c->stream))) return r;
   if ((r = upload(&c->d_chr_n, chr_n, (size_t)n_chr, c->stream))) return r;
   if ((r = upload<double>(&c->d_chr_null, nullptr, (size_t)n_chr, c->stream))) return r;
+  if ((r = upload<double>(&c->d_win_null, nullptr, (size_t)n_snps, c->stream))) return r;
+  c->win_valid = false; c->win_er = -1;
   c->n_snps = n_snps; c->n_chr = n_chr;
   c->h_chr_n.assign(chr_n, chr_n + n_chr);
   c->h_chr_start.assign(chr_start, chr_start + n_chr);
@@ -959,6 +1030,7 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
 int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
   if (!c || !c->d_pr) return set_err(FSCLG_E_STATE, "snps not uploaded");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  c->win_valid = false;
   if (!row) HIPCHK(hipMemcpyAsync(c->d_pr, c->d_pr0, sizeof(uint2) * c->n_snps, hipMemcpyDeviceToDevice, c->stream), "copy rows");
   else {
     c->h_stage.resize(c->n_snps);
@@ -1009,6 +1081,68 @@ static int ensure_io(fsclg_ctx* c, int n) {
   return FSCLG_OK;
 }
 
+// the null sums of every window of the chromosomes longer than 2*er+1 SNPs, for the
+// current rows (window_null_kernel, on the search stream, timed apart from the search)
+static int ensure_windows(fsclg_ctx* c, int er) {
+  const long long W = 2ll * er + 1;
+  if (c->win_valid && c->win_er == er) return FSCLG_OK;
+  if (c->win_er != er) {
+    std::vector<int2> tasks;
+    for (int ch = 0; ch < c->n_chr; ch++) {
+      const long long n = c->h_chr_n[ch];
+      if (n <= W) continue;
+      const int cnt = (int)(n - W + 1);  // window starts cs .. ce - 2er
+      for (int o = 0; o < cnt; o += WN_WG * WN_PER)
+        tasks.push_back(make_int2(c->h_chr_start[ch] + o, std::min(WN_WG * WN_PER, cnt - o)));
+    }
+    c->n_wtasks = (int)tasks.size();
+    if (c->n_wtasks > c->wtask_cap) {
+      if (c->d_wtasks) hipFree(c->d_wtasks);
+      c->d_wtasks = nullptr; c->wtask_cap = 0;
+      HIPCHK(hipMalloc((void**)&c->d_wtasks, sizeof(int2) * c->n_wtasks), "hipMalloc window tasks");
+      c->wtask_cap = c->n_wtasks;
+    }
+    if (c->n_wtasks)
+      HIPCHK(hipMemcpyAsync(c->d_wtasks, tasks.data(), sizeof(int2) * tasks.size(), hipMemcpyHostToDevice, c->stream),
+             "copy window tasks");
+    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    c->win_er = er;
+  }
+  if (c->n_wtasks) {
+    HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
+    hipLaunchKernelGGL(window_null_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->stream, c->d_pr, c->d_null,
+                       c->d_wtasks, (int)W, c->d_win_null);
+    HIPCHK(hipGetLastError(), "launch window_null_kernel");
+    HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
+    HIPCHK(hipEventSynchronize(c->ev1), "hipEventSynchronize");
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
+    c->window_ms += ms;
+  }
+  c->win_valid = true;
+  return FSCLG_OK;
+}
+
+// the best window of K = room / (rows * 32) intervals for a histogram of terms per interval.
+// Every row is held: a miss sends the whole wave's gather to the global table, so a row
+// prefix (a per-lane miss rate) would miss in nearly every wave, while an interval window
+// misses in whole waves (neighbouring sites have nearly equal log distance).
+static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
+  c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
+  const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
+  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8;
+  const int K = room < 0 ? 0 : std::min(c->n_iv, room / ((c->n_rows + 1) * 32));
+  double htot = 0.0;
+  for (double h : hist) htot += h;
+  if (K <= 0 || htot <= 0) return;
+  std::vector<double> hpre(c->n_iv + 1, 0.0);
+  for (int j = 0; j < c->n_iv; j++) hpre[j + 1] = hpre[j] + hist[j];
+  int bj = 0;
+  for (int j = 0; j + K <= c->n_iv; j++) if (hpre[j + K] - hpre[j] > hpre[bj + K] - hpre[bj]) bj = j;
+  c->c_ivc0 = bj; c->c_civ = K; c->c_crow = c->n_rows + 1;
+  c->c_cover = (hpre[bj + K] - hpre[bj]) / htot;
+}
+
 // Choose the LDS coefficient window: intervals [ivc0, ivc0 + K) x device rows [0, R) with
 // K * R * 32 bytes beside the static LDS, thresholds and null rows in LDS_WG, maximising
 // the expected share of terms it serves = (share of sites in rows < R) x (share of terms
@@ -1045,26 +1179,8 @@ static void plan_cache(fsclg_ctx* c) {
         }
     }
   }
-  double htot = 0.0;
-  for (double h : hist) htot += h;
-  long long rtot = 0;
-  for (long long n : c->h_row_cnt) rtot += n;
-  if (htot <= 0 || rtot <= 0) return;
-  std::vector<double> hpre(c->n_iv + 1, 0.0);
-  for (int j = 0; j < c->n_iv; j++) hpre[j + 1] = hpre[j] + hist[j];
-  // every row: a miss sends the whole wave's gather to the global table, so a row prefix
-  // (a per-lane miss rate) would miss in nearly every wave, while an interval window
-  // misses in whole waves (neighbouring sites have nearly equal log distance)
-  const int nrow = c->n_rows + 1;
-  long long rcum = rtot;
-  for (int R = nrow; R <= nrow; R++) {
-    const int K = std::min(c->n_iv, room / (R * 32));
-    if (K <= 0) break;
-    int bj = 0;
-    for (int j = 0; j + K <= c->n_iv; j++) if (hpre[j + K] - hpre[j] > hpre[bj + K] - hpre[bj]) bj = j;
-    const double cover = ((double)rcum / rtot) * ((hpre[bj + K] - hpre[bj]) / htot);
-    if (cover > c->c_cover) { c->c_cover = cover; c->c_ivc0 = bj; c->c_civ = K; c->c_crow = R; }
-  }
+  choose_window(c, hist);
+  c->hist_pending = true;  // the first launch measures the real histogram (refine grids follow the data)
 }
 
 static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
@@ -1077,9 +1193,9 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
   P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; P.civ_max = std::max(c->c_civ - 1, 0);
   P.n_cache = P.n_civ * P.stride;
   P.off_b = P.n_cache * 16; P.off_thr = 2 * P.off_b; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
-  P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null;
+  P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null; P.win_null = c->d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
-  P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats; P.ctrace = nullptr;
+  P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   if (getenv("FSCLG_CELL_TRACE")) {
     if (c->ctrace_cap < n) {
       if (c->d_ctrace) hipFree(c->d_ctrace);
@@ -1122,13 +1238,12 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
   if (eval_range < 0 || bp_resl < 0) return set_err(FSCLG_E_ARG, "eval_range/bp_resl");
   for (int i = 0; i < n_cells; i++) {
     if (cells[i].chr < 0 || cells[i].chr >= c->n_chr) return set_err(FSCLG_E_ARG, "cell chromosome");
-    const long long nchr = c->h_chr_n[cells[i].chr];
-    if (nchr > 2ll * eval_range + 1)
-      return set_err(FSCLG_E_UNSUPPORTED, "chromosome larger than 2*eval_range+1 SNPs (windowed null sums)");
-    if (nchr > (long long)MAXSEG_W * SEG) return set_err(FSCLG_E_UNSUPPORTED, "window above 196608 SNPs");
+    const long long nwin = std::min((long long)c->h_chr_n[cells[i].chr], 2ll * eval_range + 1);
+    if (nwin / SEG + 2 > (long long)MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
   }
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
+  if ((r = ensure_windows(c, eval_range))) return r;
   if ((r = ensure_io(c, n_cells))) return r;
   // longest first: each cell's cost in its last launch (permutation trials repeat the cells),
   // else a guess (cells nearer the middle of a chromosome walk further on both sides)
@@ -1153,7 +1268,44 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
   HIPCHK(hipMemcpyAsync(c->d_cells, c->h_cells.data(), sizeof(fsclg_cell_t) * n_cells, hipMemcpyHostToDevice, c->stream),
          "copy cells");
   Params P = make_params(c, n_cells, 0, eval_range, bp_resl);
+  if (c->hist_pending && P.n_civ > 0) {
+    if (c->ivhist_n < c->n_iv) {
+      if (c->d_ivhist) hipFree(c->d_ivhist);
+      c->d_ivhist = nullptr; c->ivhist_n = 0;
+      HIPCHK(hipMalloc((void**)&c->d_ivhist, sizeof(unsigned long long) * c->n_iv), "hipMalloc ivhist");
+      c->ivhist_n = c->n_iv;
+    }
+    HIPCHK(hipMemsetAsync(c->d_ivhist, 0, sizeof(unsigned long long) * c->n_iv, c->stream), "hipMemset ivhist");
+    P.ivhist = c->d_ivhist;
+  }
   if ((r = launch(c, P, n_cells))) return r;
+  if (P.ivhist) {  // re-plan the LDS window from the measured histogram
+    std::vector<unsigned long long> h(c->n_iv);
+    HIPCHK(hipMemcpyAsync(h.data(), P.ivhist, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream),
+           "copy ivhist");
+    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    choose_window(c, std::vector<double>(h.begin(), h.end()));
+    c->hist_pending = false;
+    if (getenv("FSCLG_DEBUG_PLAN")) {  // development aid: coverage of the best window by size
+      double tot = 0;
+      for (auto v : h) tot += (double)v;
+      fprintf(stderr, "fsclg plan: window [%d, %d) covers %.3f\n", c->c_ivc0, c->c_ivc0 + c->c_civ, c->c_cover);
+      for (int K : {8, 16, 21, 32, 48, 64, 96, 128}) {
+        double best = 0, run = 0;
+        for (int j = 0; j < c->n_iv; j++) {
+          run += (double)h[j];
+          if (j >= K) run -= (double)h[j - K];
+          best = std::max(best, run);
+        }
+        fprintf(stderr, "  K=%3d covers %.3f\n", K, best / tot);
+      }
+      for (int j = 0; j < c->n_iv; j += 10) {
+        double sub = 0;
+        for (int k = j; k < std::min(j + 10, c->n_iv); k++) sub += (double)h[k];
+        fprintf(stderr, "  iv %3d..%3d: %.3f\n", j, j + 9, sub / tot);
+      }
+    }
+  }
   if (P.ctrace) {  // development aid: append [n, then n x (start, end, cu, terms)] to the file
     std::vector<unsigned long long> h((size_t)4 * n_cells);
     HIPCHK(hipMemcpyAsync(h.data(), P.ctrace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream),
@@ -1192,7 +1344,7 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
     if (p.window_start < 0 || p.window_end >= c->n_snps || p.window_start > p.window_end ||
         p.nearest_snp < p.window_start || p.nearest_snp > p.window_end)
       return set_err(FSCLG_E_ARG, "point window");
-    if (p.window_end - p.window_start + 1 > MAXSEG_W * SEG) return set_err(FSCLG_E_UNSUPPORTED, "window above 196608 SNPs");
+    if ((p.window_end - p.window_start + 1) / SEG + 2 > MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
   }
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
@@ -1224,7 +1376,7 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
   memset(st, 0, sizeof *st);
   st->n_terms = h[0]; st->n_null = h[1]; st->n_walks = h[2]; st->n_maxalpha = h[3];
   st->n_unsafe = h[4]; st->n_slow = h[5]; st->n_ties = h[6]; st->n_cells = h[7];
-  st->kernel_ms = c->kernel_ms; st->n_launches = c->launches;
+  st->kernel_ms = c->kernel_ms; st->n_launches = c->launches; st->window_ms = c->window_ms;
   if (c->plan_dirty) plan_cache(c);
   st->cache_iv0 = c->c_ivc0; st->cache_n_iv = c->c_civ; st->cache_n_rows = c->c_crow; st->cache_cover = c->c_cover;
   return FSCLG_OK;
@@ -1234,7 +1386,7 @@ int fsclg_reset_stats(fsclg_ctx* c) {
   if (!c) return set_err(FSCLG_E_ARG, "stats");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
-  c->kernel_ms = 0.0; c->launches = 0;
+  c->kernel_ms = 0.0; c->launches = 0; c->window_ms = 0.0;
   return FSCLG_OK;
 }
 

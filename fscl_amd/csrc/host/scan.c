@@ -334,7 +334,8 @@ static void eval_cells(const fsclg_cell_t *cells, int n, int eval_range, int bp_
   int lo = 0, hi = n, i, r;
   if (D.world > 1) {
     cost = fh_malloc(sizeof(double) * (n ? n : 1), "cost");
-    for (i = 0; i < n; i++) cost[i] = (double)D.chr_n[cells[i].chr];
+    for (i = 0; i < n; i++) /* a cell's work scales with its window */
+      cost[i] = (double)(D.chr_n[cells[i].chr] < 2 * eval_range + 1 ? D.chr_n[cells[i].chr] : 2 * eval_range + 1);
     rank_share(cost, n, &lo, &hi);
     memset(out, 0, sizeof(fsclg_point_t) * n);
   }
@@ -343,9 +344,6 @@ static void eval_cells(const fsclg_cell_t *cells, int n, int eval_range, int bp_
     DBG("search_maxpos: %d cells from %d\n", m, i);
     r = fsclg_search_maxpos(D.ctx, cells + i, m, eval_range, bp_resl, out + i);
     DBG("search_maxpos: done (%d)\n", r);
-    if (r == FSCLG_E_UNSUPPORTED)
-      logmsg(MSG_FATAL, "fscl_amd: %s. Chromosomes above %d SNPs need per-window null sums, which this "
-                        "build does not evaluate on the GPU yet.", fsclg_last_error(), 2 * eval_range + 1);
     dev_check(r, "search_maxpos");
   }
   D.st.gp_evals += (unsigned long long)(hi - lo);
@@ -655,7 +653,7 @@ void fscl_amd_get_stats(fscl_amd_stats_t *st) {
       st->n_terms = g.n_terms; st->n_null = g.n_null; st->n_walks = g.n_walks; st->n_maxalpha = g.n_maxalpha;
       st->n_unsafe = g.n_unsafe; st->n_slow = g.n_slow; st->n_ties = g.n_ties; st->n_launches = g.n_launches;
       st->cache_iv0 = g.cache_iv0; st->cache_n_iv = g.cache_n_iv; st->cache_n_rows = g.cache_n_rows;
-      st->cache_cover = g.cache_cover;
+      st->cache_cover = g.cache_cover; st->window_ms = g.window_ms;
     }
   }
 }

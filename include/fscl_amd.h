@@ -168,6 +168,7 @@ typedef struct {
   int trials;             /* permutation trials run */
   int cache_iv0, cache_n_iv, cache_n_rows;  /* LDS coefficient window (fsclg_stats_t) */
   double cache_cover;
+  double window_ms;       /* window null-sum kernels (chromosomes above 2*eval_range+1 SNPs) */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

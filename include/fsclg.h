@@ -65,6 +65,7 @@ typedef struct {
   unsigned long long n_launches;
   int cache_iv0, cache_n_iv, cache_n_rows;  /* LDS coefficient window: intervals, device rows */
   double cache_cover;              /* its planned share of the terms */
+  double window_ms;                /* summed duration of the window null-sum kernels (HIP events) */
 } fsclg_stats_t;
 
 int fsclg_open(int device, fsclg_ctx **out);

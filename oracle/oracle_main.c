@@ -52,6 +52,7 @@ int main(int argc, char **argv) {
         {0, "no-scan", &no_scan, T_FLAG},
         {0, "ascbias-background-only", &o.ascbias_background_only, T_FLAG},
         {0, "dump-points", &dump, T_STR}, /* oracle only: hex-float dump of every point */
+        {0, "eval-range", &o.eval_range, T_INT}, /* oracle only: scan_chromosome's eval_range (fscl.c:175 fixes 81920) */
         {0, NULL, NULL, 0}};
     i = 1;
     while (i < argc) {

@@ -85,6 +85,34 @@ def test_gpu_matches_oracle(built, tmp, name, gen, opts):
     assert st["n_terms"] > 0
 
 
+@pytest.mark.parametrize("name,er,parts,opts", [
+    # every chromosome longer than the window 2*er+1: per-window null sums on the device
+    ("long", 300, [dict(n_chr=2, chr_len=4_000_000, snps_per_chr=4000, n=30, seed=51, sweeps_per_chr=1)],
+     ["--coarse-grid-spacing=40000", "--n-permute=4"]),
+    # a mix: chromosomes shorter than, equal to and longer than the window, two depths
+    ("mixed", 700, [dict(n_chr=1, chr_len=900_000, snps_per_chr=900, n=24, seed=52, chr_names=["a"]),
+                    dict(n_chr=1, chr_len=1_500_000, snps_per_chr=1401, n=24, seed=53, chr_names=["b"]),
+                    dict(n_chr=1, chr_len=9_000_000, snps_per_chr=7000, n=24, seed=54, chr_names=["c"],
+                         sweeps_per_chr=2, missing=0.2, max_missing=2)],
+     ["--coarse-grid-spacing=30000", "--n-permute=3"]),
+])
+def test_windowed_null_sums_match_oracle(built, tmp, name, er, parts, opts):
+    """Chromosomes above 2*eval_range+1 SNPs: each point's null_logl is its own window's
+    sequential sum (scan-chromosome.c:92-94), recomputed on the device for every trial."""
+    snp = tmp / f"{name}.snp"
+    chrs = []
+    for p in parts:
+        chrs += synth.generate(**p)
+    synth.write_snp_file(str(snp), chrs)
+    run_oracle(snp, tmp / "o.txt", [*opts, f"--eval-range={er}"], tmp / "o.dump",
+               threads=min(16, os.cpu_count() or 1))
+    fscl_amd.reset_stats()
+    scan = fscl_amd.run(snp, tmp / "g.txt", eval_range=er, **_kw(opts))
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), name)
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+    assert fscl_amd.get_stats()["window_ms"] > 0
+
+
 def test_ms_input_matches_oracle_on_converted_file(built, tmp):
     ms = tmp / "x.ms"
     synth.write_ms_file(str(ms), n_blocks=4, n_hap=20, n_seg=600, seed=41)

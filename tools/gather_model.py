@@ -74,3 +74,30 @@ for K in (10, 16, 21, 32, 43, 64):
     c = np.convolve(hist, np.ones(K, np.int64), mode="valid")
     b = int(np.argmax(c))
     print(f"  K={K:3d}: best window [{b},{b + K}) covers {c[b] / tot:.3f}; top-K set covers {cum[K - 1]:.3f}")
+
+# wave-level hit/miss for a given window (argv[2], argv[3])
+if len(sys.argv) > 3:
+    w0, K = int(sys.argv[2]), int(sys.argv[3])
+    anyhit = anymiss = both = wv = 0
+    lanes_hit = lanes = 0
+    for g in rng.integers(0, pos[-1], size=24):
+        near = int(np.clip(np.searchsorted(pos, g), 0, len(pos) - 1))
+        for la in las:
+            ad = np.abs(pos - g)
+            x = np.log(np.maximum(ad, 1)) + la
+            ok = x <= LOG_AD_MAX
+            lo = near
+            while lo > 0 and ok[lo - 1]:
+                lo -= 1
+            hi = near
+            while hi < len(pos) - 1 and ok[hi + 1]:
+                hi += 1
+            iv = np.clip(((x[lo:hi + 1] - LOG_AD_MIN) / step).astype(np.int64), 0, n_iv - 1)
+            hit = (iv >= w0) & (iv < w0 + K)
+            for j in range(0, len(iv), 64):
+                h = hit[j:j + 64]
+                wv += 1
+                anyhit += h.any(); anymiss += (~h).any(); both += h.any() and (~h).any()
+                lanes_hit += h.sum(); lanes += len(h)
+    print(f"window [{w0},{w0 + K}): lane hit {lanes_hit / lanes:.3f}; waves any-hit {anyhit / wv:.3f} "
+          f"any-miss {anymiss / wv:.3f} both {both / wv:.3f}")
