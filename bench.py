@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--traffic-summary", default=None,
+                    help="rocprofv3 PMC summary (tools/prof_summary.py) for roofline.traffic; default: newest in profiles/")
     return ap.parse_args()
 
 
@@ -141,6 +143,20 @@ def main() -> int:
     achieved = alg_bytes / kernel_s / 1e9 if kernel_s > 0 else 0.0
     fp64 = FLOPS_PER_TERM * st["n_terms"] / kernel_s / 1e12 if kernel_s > 0 else 0.0
 
+    # HBM traffic per launch of the same kernel from separate rocprofv3 --pmc passes
+    # (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), committed under profiles/
+    traffic, traffic_src = None, None
+    cands = [Path(args.traffic_summary)] if args.traffic_summary else sorted(
+        (ROOT / "profiles").glob("*_summary.json"), key=lambda q: q.stat().st_mtime)
+    for q in reversed(cands):
+        try:
+            t = json.loads(q.read_text()).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            continue
+        if t:
+            traffic, traffic_src = float(t), str(q.relative_to(ROOT) if q.is_absolute() else q)
+            break
+
     out = {
         "metric": METRIC,
         "value": units / elapsed,
@@ -159,7 +175,7 @@ def main() -> int:
                    "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"] * world,
                    "units_per_step": units / args.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "search_maxpos_kernel", "alg_bytes_per_launch": alg_bytes / launches,
                      "avg_launch_ms": st["kernel_ms"] / launches, "launches": st["n_launches"],
                      "fp64_tflops": fp64, "fp64_frac": fp64 / FP64_PEAK_TFS},
