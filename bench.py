@@ -147,7 +147,7 @@ def main() -> int:
     # (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), committed under profiles/
     traffic, traffic_src = None, None
     cands = [Path(args.traffic_summary)] if args.traffic_summary else sorted(
-        (ROOT / "profiles").glob("*_summary.json"), key=lambda q: q.stat().st_mtime)
+        (ROOT / "profiles").glob("r*_summary.json"))  # round-tagged names sort in round order
     for q in reversed(cands):
         try:
             t = json.loads(q.read_text()).get("hbm_bytes_per_launch")
