@@ -67,6 +67,9 @@ constexpr int LDS_WG = FSCLG_LDS_WG;  // LDS per workgroup (default: two workgro
 constexpr int U = FSCLG_U;         // terms per lane per loop trip (independent load chains)
 constexpr double LOG_AD_MIN = -20.0;  // fscl.h:79
 constexpr double LOG_AD_MAX = 4.0;    // fscl.h:80
+constexpr int BLK_LOG = 10, BLK = 1 << BLK_LOG;  // row-sorted site blocks (Params.prs)
+constexpr int SORT_MIN = 16 * BLK;    // walks this long use the row-sorted blocks
+constexpr int TIE_FIX = 1 << 25;      // tie record flag: in-segment prefix parity still to compute
 constexpr int PAD = 1024;             // slack after pos/row: a trip may read up to 64*U past a walk's end
 constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsigned order = signed order
 
@@ -74,6 +77,8 @@ enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2 };
 
 struct Params {
   const uint2* pr;             // [n_snps + PAD] (position ^ POS_BIAS, device row = caller's row + 1; 0: zero sentinel)
+  const uint2* prs;            // [blocks * BLK + PAD] the same sites, each aligned BLK-block sorted by row:
+                               // (position ^ POS_BIAS, row | offset in block << 16); null: no sorted path
   const double* logt3;         // [3][65536]: c_b + log_table[i], the three branches of sm-search.c:40-46
   const double* coef;          // [n_iv][n_rows + 1][4], device row 0 all zero (sentinel)
   const double* nullrow;       // [n_rows + 1], entry 0 zero
@@ -88,7 +93,7 @@ struct Params {
   const fsclg_cell_t* cells;
   fsclg_point_t* out;
   unsigned long long* stats;   // 8 counters
-  unsigned long long* ctrace;  // optional per-cell [start, end, cu id, terms] (FSCLG_CELL_TRACE)
+  unsigned long long* ctrace;  // optional per-cell [start, end, cu id, terms, phase ticks x4] (FSCLG_CELL_TRACE)
   unsigned long long* ivhist;  // optional [n_iv]: terms per spline interval, one sample per segment
   int n_coarse;
   int n_iv;
@@ -101,6 +106,7 @@ struct Params {
   int n_civ, civ_max;          // civ_max = max(n_civ - 1, 0)
   int n_cache;                 // n_civ * stride blocks
   int off_b, off_thr, off_nul; // byte offsets in fsclg_dyn (plane A at 0)
+  int off_lt, lt_hi;           // LDS copy of logt3 branch 2 (|d| > 2^24) entries [256, lt_hi) at off_lt; lt_hi 0: none
   int eval_range;
   int bp_resl;
   int n_cells;
@@ -117,8 +123,12 @@ struct Walk {
   int nl, nr;     // terms left / right of the nearest SNP
   int len;        // 0 (nearest already outside log(ad) <= 4) or 1 + nl + nr
   int seg0;       // first global segment id
-  int nseg;       // left-part segments then right-part segments (seg_range)
+  int nseg;       // left-part segments then right-part segments (seg_bounds)
+  int nsl;        // left-part segments
+  int srt;        // segments are row-sorted blocks (prs)
+  int wb;         // LDS coefficient window base for this walk
   double la;
+  double xl, xr;  // log(alpha d) at the walk's far ends (the walk's largest x is one of them)
 };
 
 struct Smem {
@@ -140,6 +150,13 @@ struct Smem {
   int n_slow;
   int best[3];
   unsigned long long cnt[8];
+  int ivc0;                       // base interval of the coefficient window now in LDS
+  int ngrp;                       // walk groups of the phase (one LDS window each), in segment order
+  int gwb[MAXWALK];
+  int gseg[MAXWALK + 1];
+  int word[MAXWALK];              // walks in segment order
+  int hkey;                       // interval-histogram key of the phase: 0 coarse, 1 + c refine around coarse c
+  unsigned long long tph[4];      // FSCLG_PHASE_TIMING: wall-clock ticks in bounds / layout / segments / resolve
 };
 
 // dynamic LDS of a workgroup (LDS = true): coefficient planes of the top K intervals, the
@@ -158,6 +175,19 @@ __device__ __forceinline__ double logt_dev(uint32_t ad, const double* __restrict
   const uint32_t sh = ad > 0xFFFFFFu ? 16u : (ad > 0xFFFFu ? 8u : 0u);
   const uint32_t ix = (ad >> sh) + (sh << 13);  // + 65536 * branch
   return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(LT3) + (ix << 3));
+}
+
+// logt_dev with the far branch (|d| > 2^24: log_table[|d| >> 16] + c_2, where most terms of
+// the long walks fall) read from the workgroup's LDS copy; lanes outside it (and the rare
+// entries past lt_hi) take the global table
+template <bool LDS>
+__device__ __forceinline__ double logt_lds(uint32_t ad, const Params& P) {
+  if constexpr (LDS) {
+    const uint32_t i2 = ad >> 16;
+    if (ad > 0xFFFFFFu && i2 < (uint32_t)P.lt_hi)
+      return reinterpret_cast<const double*>(fsclg_dyn + P.off_lt)[i2 - 256u];
+  }
+  return logt_dev(ad, P.logt3);
 }
 
 // |pos_i - sweep| from biased positions: one v_sad_u32
@@ -195,6 +225,9 @@ __device__ __forceinline__ double null_of(uint32_t r, const Smem& S, const Param
 // wave (neighbouring sites, nearly equal log distance) read from one interval's rows;
 // 32-bit byte offset (the table is < 4 GiB, checked on upload)
 __device__ __forceinline__ const double2* coef_of(uint32_t r, int iv, const Params& P) {
+#ifdef FSCLG_EXP_COEFCONST  // timing ablation only (wrong results): one block per interval parity
+  return reinterpret_cast<const double2*>(P.coef) + (iv & 1) * 2;
+#endif
   const uint32_t off = (__umul24((uint32_t)iv, (uint32_t)P.stride) + r) << 5;
   return reinterpret_cast<const double2*>(reinterpret_cast<const char*>(P.coef) + off);
 }
@@ -203,13 +236,13 @@ __device__ __forceinline__ const double2* coef_of(uint32_t r, int iv, const Para
 // planes when (interval, row) lies in the cached window (planned on the host from sampled
 // walks and row frequencies, fsclg_plan_cache), from the global table otherwise
 template <bool LDS>
-__device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Params& P, double2& a, double2& b) {
+__device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, const Params& P, double2& a, double2& b) {
 #ifdef FSCLG_NOCACHE  // experiment: coefficients always from the global table
   if constexpr (false) {
 #else
   if constexpr (LDS) {
 #endif
-    const uint32_t ci = (uint32_t)(iv - P.ivc0);
+    const uint32_t ci = (uint32_t)(iv - S.ivc0);
     const bool hit = ci < (uint32_t)P.n_civ;  // every row is cached
     const uint32_t li = __umul24(min(ci, (uint32_t)P.civ_max), (uint32_t)P.stride) + r;
     a = reinterpret_cast<const double2*>(fsclg_dyn)[li];
@@ -230,7 +263,7 @@ __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Params& P, 
 // then per term the LDS window or, for lanes outside it, the global table
 template <bool LDS>
 __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t (&rv)[U], const Smem& S,
-                                           const Params& P, double2 (&ca)[U], double2 (&cb)[U]) {
+                                           const Params& P, int ivc0, double2 (&ca)[U], double2 (&cb)[U]) {
 #ifdef FSCLG_NOCACHE
   constexpr bool CACHE = false;
 #else
@@ -242,7 +275,7 @@ __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t 
   if constexpr (CACHE) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint32_t ci = (uint32_t)(iv[u] - P.ivc0);
+      const uint32_t ci = (uint32_t)(iv[u] - ivc0);
       if (ci < (uint32_t)P.n_civ) {  // every row is cached
         const uint32_t li = __umul24(ci, (uint32_t)P.stride) + rv[u];
         ca[u] = reinterpret_cast<const double2*>(fsclg_dyn)[li];
@@ -270,7 +303,7 @@ __device__ __forceinline__ double term_dev(int i, int sweep, double la, const Sm
   const int iv = interval_of<LDS>(x, S, P);
   const uint32_t r = P.pr[i].y;
   double2 a, b;
-  coef_fetch<LDS>(r, iv, P, a, b);
+  coef_fetch<LDS>(r, iv, S, P, a, b);
   const double y = x * (a.x * x * x + a.y * x + b.x) + b.y;
   return y - null_of<LDS>(r, S, P);
 }
@@ -286,7 +319,7 @@ __device__ __forceinline__ long long wave_sum64(long long v) {
 }
 
 // init_scan_result (scan-chromosome.c:58-101) for one point, one thread
-__device__ void init_point(Pt& pt, int chr, int pos, const Params& P) {
+__device__ __forceinline__ void init_point(Pt& pt, int chr, int pos, const Params& P) {
   const int a = P.chr_start[chr], n = P.chr_n[chr];
   int i = 0, j = n;
   while (j - i > 1) {  // search_snppos, scan-chromosome.c:39-56
@@ -331,7 +364,7 @@ __device__ __forceinline__ void set_binade(Pt& pt) {
 }
 
 // the walk's index range: monotone predicate log(alpha d) > 4 on each side
-__device__ void walk_bounds(Walk& W, const Pt& pt, const Params& P, int side) {
+__device__ __forceinline__ void walk_bounds(Walk& W, const Pt& pt, const Params& P, int side) {
   const int near = pt.nearest, sweep = pt.sweep;
   const double la = W.la;
   if (side == 0) {
@@ -346,6 +379,7 @@ __device__ void walk_bounds(Walk& W, const Pt& pt, const Params& P, int side) {
       }
     }
     W.nl = near - b;
+    W.xl = log_ad_of(b < near ? b : near, sweep, la, P);
   } else {
     // right: first element may violate alone (de-collision shift), otherwise the ok-set is a prefix
     int r = near;
@@ -358,12 +392,13 @@ __device__ void walk_bounds(Walk& W, const Pt& pt, const Params& P, int side) {
       r = a;
     }
     W.nr = r - near;
+    W.xr = log_ad_of(r, sweep, la, P);
   }
 }
 
 // exact sequential sum of one walk by one wave (slow path, settles an argmax)
 template <bool LDS>
-__device__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, const Params& P, int lane) {
+__device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, const Params& P, int lane) {
   double acc = pt.N;
   for (int kb = 0; kb < W.len; kb += 64) {
     const int k = kb + lane;
@@ -375,24 +410,46 @@ __device__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, co
   return acc;
 }
 
-// segment s of a walk, in index order j = i - (nearest - nl): the left part (j <= nl, the
-// nearest SNP and those before it) owns segments [0, nsl), the right part the rest, so
-// each part's k-order (sm-search.c:190-228) is monotone in j within it
-__device__ __forceinline__ int left_segs(int nl) { return (nl + SEG) / SEG; }
-__device__ __forceinline__ void seg_range(const Walk& W, int s, int& jb, int& je) {
-  const int nsl = left_segs(W.nl);
-  if (s < nsl) { jb = s * SEG; je = min(jb + SEG, W.nl + 1); }
-  else { jb = W.nl + 1 + (s - nsl) * SEG; je = min(jb + SEG, W.len); }
+// A walk covers the site indices [nearest - nl, nearest + nr]; its left part
+// [nearest - nl, nearest] (walked downwards, sm-search.c:190-228) and right part
+// [nearest + 1, nearest + nr] are cut into separate segments (left ones first), so each
+// part's walk order is monotone in the index.  Index-order walks: SEG-site segments.
+// Row-sorted walks: the part's intersections with the aligned BLK-blocks of prs.
+__device__ __forceinline__ void seg_bounds(const Walk& W, const Pt& pt, int s, int& ib, int& ie) {
+  const int lo = pt.nearest - W.nl, near = pt.nearest, hi = pt.nearest + W.nr;
+  if (!W.srt) {
+    if (s < W.nsl) { ib = lo + s * SEG; ie = min(ib + SEG, near + 1); }
+    else { ib = near + 1 + (s - W.nsl) * SEG; ie = min(ib + SEG, hi + 1); }
+  } else if (s < W.nsl) {
+    const int b = (lo >> BLK_LOG) + s;
+    ib = max(b << BLK_LOG, lo); ie = min((b + 1) << BLK_LOG, near + 1);
+  } else {
+    const int b = ((near + 1) >> BLK_LOG) + (s - W.nsl);
+    ib = max(b << BLK_LOG, near + 1); ie = min((b + 1) << BLK_LOG, hi + 1);
+  }
 }
 
-// one segment (<= 1024 terms) of one walk, by one wave, in index order: U terms per
-// lane per trip with all loads issued first; lanes past the segment read the padding
-// and take the zero sentinel row (term exactly 0).  Per lane: R = rint(t/u) summed in
-// fp64 into the wave's accumulators for this walk (acc = sum R, accm = sum |R|; exact
-// while accm < 2^51, checked when the wave flushes the walk); the segment's parity bit
-// (for the tie replay) from one ballot.
-template <bool LDS>
-__device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane, double& acc, double& accm) {
+// the segment of site index i of the walk
+__device__ __forceinline__ int seg_of(const Walk& W, const Pt& pt, int i) {
+  const int lo = pt.nearest - W.nl, near = pt.nearest;
+  if (!W.srt) return i <= near ? (i - lo) / SEG : W.nsl + (i - near - 1) / SEG;
+  return i <= near ? (i >> BLK_LOG) - (lo >> BLK_LOG) : W.nsl + (i >> BLK_LOG) - ((near + 1) >> BLK_LOG);
+}
+
+__device__ __forceinline__ bool odd_int(double v) { return v - 2.0 * floor(0.5 * v) != 0.0; }
+
+// one segment of one walk, by one wave: U terms per lane per trip with all loads issued
+// first.  Index order (SORTED = false): the segment's sites in order; lanes past it read
+// the padding.  Row-sorted (SORTED = true): the whole BLK-block of prs (neighbouring lanes
+// share rows, so the coefficient gathers touch few lines); lanes whose site lies outside
+// the segment are masked.  Masked lanes take the zero sentinel row (term exactly 0).
+// Per lane: R = rint(t/u) summed in fp64 into the wave's accumulators for this walk
+// (acc = sum R, accm = sum |R|; exact while accm < 2^51, checked when the wave flushes
+// the walk); the segment's parity bit (for the tie replay) from one ballot.  A tie on the
+// sorted path is recorded with TIE_FIX: its in-segment prefix parity (index order) is
+// computed afterwards (fix_ties).
+template <bool LDS, bool SORTED>
+__device__ __forceinline__ void run_segment(Smem& S, int w, int s, const Params& P, int lane, double& acc, double& accm) {
 #ifdef FSCLG_EXP_NOTERMS  // timing ablation only: skip every term
   return;
 #endif
@@ -400,43 +457,61 @@ __device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane, do
   const Pt& pt = S.pt[W.p];
   const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS;
   const double la = W.la, inv = pt.inv_u;
-  const uint32_t lo = (uint32_t)(pt.nearest - W.nl);
-  int jb, je;
-  seg_range(W, s, jb, je);
+  const int lo = pt.nearest - W.nl;
+  int ib, ie;
+  seg_bounds(W, pt, s, ib, ie);
+  const int n = SORTED ? BLK : ie - ib;
+  const uint32_t base = SORTED ? (uint32_t)(ib & ~(BLK - 1)) : (uint32_t)ib;
+  const uint2* src = SORTED ? P.prs : P.pr;
+  const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
   double sum = 0.0, mag = 0.0;
-  for (int kb = jb; kb < je; kb += 64 * U) {
+  for (int kb = 0; kb < n; kb += 64 * U) {
     uint32_t pv[U], rv[U];
+    int orig[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint32_t i = lo + (uint32_t)(kb + 64 * u + lane);
-      const uint2 v = ld_pr(P.pr, i);
+      const int k = kb + 64 * u + lane;
+      const uint2 v = ld_pr(src, base + (uint32_t)k);
       pv[u] = v.x;
-      rv[u] = v.y;
+      if constexpr (SORTED) {
+        orig[u] = (int)base + (int)(v.y >> 16);
+        rv[u] = (orig[u] >= ib && orig[u] < ie) ? (v.y & 0xFFFFu) : 0u;  // zero sentinel row outside
+      } else {
+        orig[u] = ib + k;
+        rv[u] = k < n ? v.y : 0u;  // zero sentinel row past the segment
+      }
     }
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (kb + 64 * u + lane >= je) rv[u] = 0u;  // zero sentinel row
     double x[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) x[u] = logt_dev(absdist(pv[u], usweep), P.logt3) + la;
-    if (P.ivhist && kb == jb && lane == 0)  // one sample per segment, weighted by its terms
-      atomicAdd(&P.ivhist[interval_of<LDS>(x[0], S, P)], (unsigned long long)(je - jb));
+    for (int u = 0; u < U; u++) {
+#ifdef FSCLG_EXP_LTCONST  // timing ablation only (wrong results): the gather hits 8 table entries
+      x[u] = P.logt3[absdist(pv[u], usweep) & 7] + la;
+#else
+      x[u] = logt_lds<LDS>(absdist(pv[u], usweep), P) + la;
+#endif
+    }
+    if (P.ivhist && kb == 0 && lane == 0)  // one sample per segment, weighted by its terms
+      atomicAdd(&P.ivhist[S.hkey * P.n_iv + interval_of<LDS>(x[0], S, P)], (unsigned long long)(ie - ib));
     double2 ca[U], cb[U];
-    coef_stage<LDS>(x, rv, S, P, ca, cb);
+    coef_stage<LDS>(x, rv, S, P, ivc0, ca, cb);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
       const double q = (y - null_of<LDS>(rv[u], S, P)) * inv;
       const double R = rint(q);                 // the even neighbour at a tie; the resolver settles ties
       const double fr = q - R;
-      if (__ballot(fabs(fr) == 0.5)) {          // rare: record the tie with its in-segment prefix parity
-        const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-        const unsigned long long ps = __ballot(sum - 2.0 * floor(0.5 * sum) != 0.0);
-        const unsigned long long pr = __ballot(R - 2.0 * floor(0.5 * R) != 0.0);
+      if (__ballot(fabs(fr) == 0.5)) {          // rare: record the tie
+        int pre = 0;
+        if constexpr (!SORTED) {                // in-segment prefix parity: earlier trips, earlier lanes
+          const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+          const unsigned long long ps = __ballot(odd_int(sum));
+          const unsigned long long pr = __ballot(odd_int(R));
+          pre = (__popcll(ps) + __popcll(pr & below)) & 1;
+        }
         if (fabs(fr) == 0.5) {
-          const int pre = (__popcll(ps) + __popcll(pr & below)) & 1;
           const int ti = atomicAdd(&S.n_ties, 1);
-          if (ti < MAXTIES) S.ties[ti] = (w << 20) | ((fr < 0.0 ? 1 : 0) << 19) | (pre << 18) | (kb + 64 * u + lane);
+          if (ti < MAXTIES)
+            S.ties[ti] = (SORTED ? TIE_FIX : 0) | (w << 20) | ((fr < 0.0 ? 1 : 0) << 19) | (pre << 18) | (orig[u] - lo);
         }
       }
       sum += R;
@@ -445,16 +520,38 @@ __device__ void run_segment(Smem& S, int w, int s, const Params& P, int lane, do
   }
   // the segment's parity: sum over lanes of (sum mod 2); partials are exact integers
   // whenever the walk passes its flush check (otherwise its value is discarded)
-  const unsigned long long odd = __ballot(sum - 2.0 * floor(0.5 * sum) != 0.0);
+  const unsigned long long odd = __ballot(odd_int(sum));
   if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
   acc += sum;
   accm += mag;
 }
 
+// the in-segment prefix parity (index order) of the ties found on the sorted path: one
+// wave per tie re-evaluates R = rint(t/u) of the segment's sites before it, with the same
+// arithmetic as run_segment
+template <bool LDS>
+__device__ __forceinline__ void fix_ties(Smem& S, const Params& P, int wave, int lane) {
+  const int nt = __builtin_amdgcn_readfirstlane(S.n_ties < MAXTIES ? S.n_ties : MAXTIES);
+  for (int t = wave; t < nt; t += NWAVE) {
+    const int v = __builtin_amdgcn_readfirstlane(S.ties[t]);
+    if (!(v & TIE_FIX)) continue;
+    const int w = (v >> 20) & 31;
+    const Walk& W = S.w[w];
+    const Pt& pt = S.pt[W.p];
+    const int it = pt.nearest - W.nl + (v & 0x3FFFF);
+    int ib, ie;
+    seg_bounds(W, pt, seg_of(W, pt, it), ib, ie);
+    int par = 0;
+    for (int i = ib + lane; i < it; i += 64) par ^= odd_int(rint(term_dev<LDS>(i, pt.sweep, W.la, S, P) * pt.inv_u));
+    par = __popcll(__ballot(par != 0)) & 1;
+    if (lane == 0) S.ties[t] = (v & ~(TIE_FIX | (1 << 18))) | (par << 18);
+  }
+}
+
 // a wave's share of walk w: int64 totals of sum R and sum |R| into S.P / S.Q.  Exact when
 // every lane's |R| total is below 2^51 (then all fp64 partials were exact, fl being
 // monotone; NaN fails the test); 8 waves x 64 lanes keep the walk's totals below 2^60.
-__device__ void flush_walk(Smem& S, int w, double acc, double accm, int lane) {
+__device__ __forceinline__ void flush_walk(Smem& S, int w, double acc, double accm, int lane) {
   const bool big = !(accm < 2251799813685248.0);  // 2^51
   const long long isum = wave_sum64(big ? 0 : (long long)acc);
   const long long imag = wave_sum64(big ? 0 : (long long)accm);
@@ -469,7 +566,7 @@ __device__ void flush_walk(Smem& S, int w, double acc, double accm, int lane) {
 // resolve walk w's exact value (thread per walk).  S.P = sum R, S.Q = sum |R| over the walk.
 // Ties are replayed in k order: fl(acc + t) rounds to even, so where t/u = F + 1/2 an odd
 // running sum takes the other neighbour of the even R (+1 if R = F, -1 if R = F + 1).
-__device__ void resolve_walk(Smem& S, int w) {
+__device__ __forceinline__ void resolve_walk(Smem& S, int w) {
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[W.p];
   if (W.len == 0) { S.exact[w] = 1; S.val[w] = pt.N; return; }
@@ -478,13 +575,13 @@ __device__ void resolve_walk(Smem& S, int w) {
   const bool overflow = S.n_ties > MAXTIES;
   int T = 0;
   const int nt = S.n_ties < MAXTIES ? S.n_ties : MAXTIES;
-  for (int j = 0; j < nt; j++) T += ((S.ties[j] >> 20) == w);
+  for (int j = 0; j < nt; j++) T += (((S.ties[j] >> 20) & 31) == w);
   const bool big = S.wflag[w] != 0 || pt.inv_u == 0.0;
   const long long S0 = big ? 0 : (long long)(pt.N * pt.inv_u);
   const long long LO = -(1ll << 53), HI = -((1ll << 52) + 1);
   const bool safe = !big && !overflow && S0 < 0 && (S0 + Qn - T >= LO) && (S0 + Pp + T <= HI);
   if (safe) {
-    const int nl = W.nl, nsl = left_segs(nl);
+    const int nl = W.nl, nsl = W.nsl;
     auto segbit = [&](int sg) { return (int)(S.segbits[w][sg >> 5] >> (sg & 31)) & 1; };
     int lpar = 0;
     for (int sg = 0; sg < nsl; sg++) lpar ^= segbit(sg);
@@ -497,14 +594,14 @@ __device__ void resolve_walk(Smem& S, int w) {
         const int v = S.ties[j];
         const int jj = v & 0x3FFFF;
         const int k = jj <= nl ? nl - jj : jj;
-        if ((v >> 20) == w && k > prevk && k < bestk) { bestk = k; bestv = v; }
+        if (((v >> 20) & 31) == w && k > prevk && k < bestk) { bestk = k; bestv = v; }
       }
       prevk = bestk;
       // parity of the running sum before this term: S0, then the terms before it in k
       // order = (left tie) the left part after it, (right tie) the left part and the
       // right part before it; R of a tie is even, so both read lpar ^ prefix-in-part
       const int jj = bestv & 0x3FFFF;
-      const int sg = jj <= nl ? jj / SEG : nsl + (jj - nl - 1) / SEG;
+      const int sg = seg_of(W, pt, pt.nearest - nl + jj);
       int sp = 0;
       for (int t = (jj <= nl ? 0 : nsl); t < sg; t++) sp ^= segbit(t);
       const int pre = (bestv >> 18) & 1, up = (bestv >> 19) & 1;
@@ -530,8 +627,22 @@ __device__ void resolve_walk(Smem& S, int w) {
 }
 
 // evaluate S.nwalk walks (already holding p, la) -> exact values in S.val
+// stage the coefficient blocks of intervals [wb, wb + n_civ) x every row into the LDS
+// planes (all threads; the caller brackets it with barriers)
+__device__ __forceinline__ void load_window(Smem& S, const Params& P, int wb) {
+  double2* ca = reinterpret_cast<double2*>(fsclg_dyn);
+  double2* cb = reinterpret_cast<double2*>(fsclg_dyn + P.off_b);
+  const double2* src = reinterpret_cast<const double2*>(P.coef) + (size_t)wb * P.stride * 2;
+  for (int e = threadIdx.x; e < P.n_cache; e += WG) {  // the window is one contiguous run of [iv][row] blocks
+    const double2 a = src[2 * e], b = src[2 * e + 1];
+    ca[e] = a;
+    cb[e] = b;
+  }
+  if (threadIdx.x == 0) S.ivc0 = wb;
+}
+
 template <bool LDS>
-__device__ void eval_walks(Smem& S, const Params& P) {
+__device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nw = S.nwalk;
   if (tid < 2 * nw) walk_bounds(S.w[tid >> 1], S.pt[S.w[tid >> 1].p], P, tid & 1);
@@ -540,7 +651,15 @@ __device__ void eval_walks(Smem& S, const Params& P) {
     for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = 0;
   }
   if (tid == 0) S.n_ties = 0;
+#ifdef FSCLG_PHASE_TIMING
+  unsigned long long t0 = 0;
+  if (tid == 0) t0 = wall_clock64();
+#define PHASE_MARK(k) do { if (tid == 0) { const unsigned long long t1 = wall_clock64(); S.tph[k] += t1 - t0; t0 = t1; } } while (0)
+#else
+#define PHASE_MARK(k) do { } while (0)
+#endif
   __syncthreads();
+  PHASE_MARK(0);
   TRACE("  bounds done: nw=%d w0 len=%d nl=%d nr=%d\n", nw, S.w[0].len, S.w[0].nl, S.w[0].nr);
   if (tid == 0) {
     int seg = 0;
@@ -548,39 +667,89 @@ __device__ void eval_walks(Smem& S, const Params& P) {
     for (int w = 0; w < nw; w++) {
       Walk& W = S.w[w];
       W.len = W.len ? 1 + W.nl + W.nr : 0;
-      W.nseg = W.len ? left_segs(W.nl) + (W.nr + SEG - 1) / SEG : 0;
+      // the walk's window: the n_civ intervals below the one of its largest x (the site
+      // count of a long walk grows like e^x up to there)
+      const int K = P.n_civ;
+      W.wb = -1;  // empty walks sort last and open no group
+      if (LDS && K > 0 && W.len) {
+        const int top = interval_of<LDS>(fmax(W.xl, W.xr), S, P);
+        W.wb = min(max(top - K + 1, 0), P.n_iv - K);
+      }
+    }
+    // walks in descending window base; a group shares the window of its first walk and
+    // takes the following walks whose base is at most 2 below it (they lose at most their
+    // two sparsest intervals)
+    for (int w = 0; w < nw; w++) {
+      int k = w;
+      while (k > 0 && S.w[S.word[k - 1]].wb < S.w[w].wb) { S.word[k] = S.word[k - 1]; k--; }
+      S.word[k] = w;
+    }
+    S.ngrp = 0;
+    for (int k = 0; k < nw; k++) {
+      Walk& W = S.w[S.word[k]];
+      if (W.len && (S.ngrp == 0 || W.wb < S.gwb[S.ngrp - 1] - 2)) {
+        S.gwb[S.ngrp] = W.wb; S.gseg[S.ngrp] = seg; S.ngrp++;
+      }
+      W.srt = (P.prs != nullptr && W.len >= SORT_MIN) ? 1 : 0;
+      const int near = S.pt[W.p].nearest, lo = near - W.nl, hi = near + W.nr;
+      if (!W.len) { W.nsl = 0; W.nseg = 0; }
+      else if (!W.srt) { W.nsl = (W.nl + SEG) / SEG; W.nseg = W.nsl + (W.nr + SEG - 1) / SEG; }
+      else {
+        W.nsl = (near >> BLK_LOG) - (lo >> BLK_LOG) + 1;
+        W.nseg = W.nsl + (W.nr ? (hi >> BLK_LOG) - ((near + 1) >> BLK_LOG) + 1 : 0);
+      }
       W.seg0 = seg;
       seg += W.nseg;
       terms += W.len;
     }
+    S.gseg[S.ngrp] = seg;
     S.seg_total = seg;
     S.cnt[0] += terms;
     S.cnt[2] += nw;
   }
   __syncthreads();
+  PHASE_MARK(1);
   TRACE("  layout done: segs=%d\n", S.seg_total);
   // static round-robin of the equal-size segments over the waves; the loop
   // counter lives in an SGPR (a per-lane atomic-dispatch loop here was
   // miscompiled into a loop that never re-issued its atomic)
   {
-    const int total = __builtin_amdgcn_readfirstlane(S.seg_total);
-    int w = 0, cw = -1;
+    const int ngrp = __builtin_amdgcn_readfirstlane(S.ngrp);
+    int k = 0, cw = -1;
     double acc = 0.0, accm = 0.0;
-    for (int g = wave; g < total; g += NWAVE) {
-      while (w < nw - 1 && g >= S.w[w].seg0 + S.w[w].nseg) w++;  // walks own consecutive segment ranges
+    for (int gi = 0; gi < ngrp; gi++) {
+     const int gwb = __builtin_amdgcn_readfirstlane(S.gwb[gi]);
+     if (LDS && P.n_civ > 0 && gwb != __builtin_amdgcn_readfirstlane(S.ivc0)) {  // uniform over the workgroup
+       __syncthreads();
+       load_window(S, P, gwb);
+       __syncthreads();
+     }
+     const int ge = __builtin_amdgcn_readfirstlane(S.gseg[gi + 1]);
+     for (int g = __builtin_amdgcn_readfirstlane(S.gseg[gi]) + wave; g < ge; g += NWAVE) {
+      while (k < nw - 1 && g >= S.w[S.word[k]].seg0 + S.w[S.word[k]].nseg) k++;  // walks own consecutive segment ranges
+      const int w = S.word[k];
       if (w != cw) {  // the wave's segments of one walk are consecutive: flush once per walk
         if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
         cw = w; acc = 0.0; accm = 0.0;
       }
-      run_segment<LDS>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+      if (S.w[w].srt) run_segment<LDS, true>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+      else run_segment<LDS, false>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+     }
     }
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
   }
   __syncthreads();
+  if (P.prs) {
+    fix_ties<LDS>(S, P, wave, lane);
+    __syncthreads();
+  }
+  PHASE_MARK(2);
   TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk(S, tid);
   if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;
   __syncthreads();
+  PHASE_MARK(3);
+#undef PHASE_MARK
   TRACE("eval_walks: nw=%d segs=%d ties=%d\n", nw, S.seg_total, S.n_ties);
   (void)wave;
 }
@@ -591,7 +760,7 @@ __device__ void eval_walks(Smem& S, const Params& P) {
 // winning walk, PRIOR if nothing beats the prior, or AMBIG after marking every
 // inexact candidate that could still win for the sequential slow path.
 constexpr int PRIOR = -1, AMBIG = -2;
-__device__ int argmax_or_mark(Smem& S, int first, int count, double prior_val) {
+__device__ __forceinline__ int argmax_or_mark(Smem& S, int first, int count, double prior_val) {
   int bi = PRIOR;
   double bv = prior_val;
   for (int c = first; c < first + count; c++)
@@ -604,7 +773,7 @@ __device__ int argmax_or_mark(Smem& S, int first, int count, double prior_val) {
 
 // search_maxalpha for the points in slots [p0, p0+np) (sm-search.c:269-300)
 template <bool LDS>
-__device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
+__device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < np) set_binade(S.pt[p0 + tid]);
   TRACE("maxalpha: p0=%d np=%d sweep=%d N=%g\n", p0, np, S.pt[p0].sweep, S.pt[p0].N);
@@ -615,7 +784,7 @@ __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
     S.w[tid].la = P.la_coarse[a];
     S.w[tid].len = 0; S.w[tid].nl = S.w[tid].nr = 0;
   }
-  if (tid == 0) { S.nwalk = np * P.n_coarse; S.cnt[3] += np; }
+  if (tid == 0) { S.nwalk = np * P.n_coarse; S.cnt[3] += np; S.hkey = 0; }
   __syncthreads();
   for (int phase = 0; phase < 2; phase++) {
     eval_walks<LDS>(S, P);
@@ -658,6 +827,7 @@ __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
           else { pt.la = S.w[bi].la; pt.sm = S.val[bi]; ci = bi - p * P.n_coarse; }
           const int cnt = P.n_refine[ci];
           pt.pad = (nw << 8) | cnt;
+          if (p == 0) S.hkey = 1 + ci;
           for (int r = 0; r < cnt; r++, nw++) {
             S.w[nw].p = p0 + p;
             S.w[nw].la = P.la_refine[ci * MAXREF + r];
@@ -681,7 +851,7 @@ __device__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
   }
 }
 
-__device__ void write_point(fsclg_point_t& o, const Pt& pt) {
+__device__ __forceinline__ void write_point(fsclg_point_t& o, const Pt& pt) {
   o.chr = pt.chr; o.nearest_snp = pt.nearest; o.sweep_pos = pt.sweep; o.n_snps = pt.n_snps;
   o.window_start = pt.wstart; o.window_end = pt.wend; o.flags = pt.flags; o.cost = 0;
   o.lalpha = pt.la; o.null_logl = pt.N; o.sm_logl = pt.sm; o.clr = pt.clr;
@@ -697,7 +867,8 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
   const int cell = blockIdx.x;
   if (cell >= P.n_cells) return;
   if (tid < 8) S.cnt[tid] = 0;
-  if (P.ctrace && tid == 0) { P.ctrace[4 * cell] = wall_clock64(); P.ctrace[4 * cell + 2] = __smid(); }
+  if (tid < 4) S.tph[tid] = 0;
+  if (P.ctrace && tid == 0) { P.ctrace[8 * cell] = wall_clock64(); P.ctrace[8 * cell + 2] = __smid(); }
   if constexpr (LDS) {
     double* thr = reinterpret_cast<double*>(fsclg_dyn + P.off_thr);
     double* nul = reinterpret_cast<double*>(fsclg_dyn + P.off_nul);
@@ -705,14 +876,11 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
     double2* cb = reinterpret_cast<double2*>(fsclg_dyn + P.off_b);
     for (int j = tid; j <= P.n_iv; j += WG) thr[j] = P.thr[j];
     for (int j = tid; j <= P.n_rows; j += WG) nul[j] = P.nullrow[j];  // + sentinel
-    // planes [ci][row] of the cached window
-    for (int e = tid; e < P.n_cache; e += WG) {
-      const int ci = e / P.stride, r = e - ci * P.stride;
-      const double2* src = reinterpret_cast<const double2*>(P.coef) + ((size_t)(P.ivc0 + ci) * P.stride + r) * 2;
-      ca[e] = src[0];
-      cb[e] = src[1];
-    }
-  }
+    (void)ca; (void)cb;
+    load_window(S, P, P.ivc0);
+    double* lt2 = reinterpret_cast<double*>(fsclg_dyn + P.off_lt);
+    for (int j = tid; j < P.lt_hi - 256; j += WG) lt2[j] = P.logt3[2 * 0x10000 + 256 + j];
+  } else if (tid == 0) S.ivc0 = 0;
   __syncthreads();
   if (P.mode == 1) {
     if (tid == 0) {
@@ -759,7 +927,10 @@ __global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
   }
   __syncthreads();
   if (tid < 8 && S.cnt[tid]) atomicAdd(&P.stats[tid], S.cnt[tid]);
-  if (P.ctrace && tid == 0) { P.ctrace[4 * cell + 1] = wall_clock64(); P.ctrace[4 * cell + 3] = S.cnt[0]; }
+  if (P.ctrace && tid == 0) {
+    P.ctrace[8 * cell + 1] = wall_clock64(); P.ctrace[8 * cell + 3] = S.cnt[0];
+    for (int k = 0; k < 4; k++) P.ctrace[8 * cell + 4 + k] = S.tph[k];
+  }
 }
 
 // ------------------------------------------------------------ window null sums
@@ -832,6 +1003,10 @@ struct fsclg_ctx {
   uint2* d_pr = nullptr;          // (biased position, device row), n_snps + PAD
   uint2* d_pr0 = nullptr;         // the same with the unpermuted rows
   std::vector<uint2> h_pr0;
+  uint2* d_prs = nullptr;         // row-sorted BLK-blocks of d_pr (null: rows too many for 16 bits)
+  uint2* d_prs0 = nullptr;
+  std::vector<uint2> h_prs;
+  std::vector<int> h_cnt;
   int n_snps = 0;
   int32_t* d_chr_start = nullptr;
   int32_t* d_chr_n = nullptr;
@@ -844,6 +1019,7 @@ struct fsclg_ctx {
   int n_chr = 0;
   std::vector<int> h_chr_n;
   std::vector<int32_t> h_pos, h_chr_start;
+  int lt_hi = 0;                        // logt3 branch-2 entries [256, lt_hi) staged in LDS
   std::vector<long long> h_row_cnt;     // sites per device row
   std::vector<double> h_lt3;
   std::vector<uint2> h_stage;
@@ -913,6 +1089,26 @@ static double interval_threshold(int j, double step) {
   return dval(hi);
 }
 
+// each aligned BLK-block of sites sorted by device row (counting sort, stable), entries
+// (biased position, row | offset in block << 16); the tail of the last block points past
+// the sites (masked by every segment)
+static void sort_blocks(fsclg_ctx* c, const uint2* pr) {
+  const int n = c->n_snps, nb = (n + BLK - 1) / BLK, nk = c->n_rows + 1;
+  c->h_prs.assign((size_t)nb * BLK + PAD, make_uint2(POS_BIAS, 0u));
+  c->h_cnt.assign(nk + 1, 0);
+  for (int b = 0; b < nb; b++) {
+    const int b0 = b * BLK, m = std::min(BLK, n - b0);
+    std::fill(c->h_cnt.begin(), c->h_cnt.end(), 0);
+    for (int k = 0; k < m; k++) c->h_cnt[pr[b0 + k].y + 1]++;
+    for (int r = 0; r < nk; r++) c->h_cnt[r + 1] += c->h_cnt[r];
+    for (int k = 0; k < m; k++) {
+      const uint2 v = pr[b0 + k];
+      c->h_prs[b0 + c->h_cnt[v.y]++] = make_uint2(v.x, v.y | ((uint32_t)k << 16));
+    }
+    for (int k = m; k < BLK; k++) c->h_prs[b0 + k] = make_uint2(POS_BIAS, (uint32_t)k << 16);
+  }
+}
+
 extern "C" {
 
 const char* fsclg_last_error(void) { return g_err; }
@@ -944,7 +1140,7 @@ int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_ctrace, c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr, c->d_pr0, c->d_chr_start, c->d_chr_n,
+  void* ptrs[] = {c->d_ctrace, c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr, c->d_pr0, c->d_prs, c->d_prs0, c->d_chr_start, c->d_chr_n,
                   c->d_chr_null, c->d_win_null, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   hipEventDestroy(c->ev0);
@@ -1007,6 +1203,19 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   for (int i = 0; i < n_snps; i++) pr[i] = make_uint2((uint32_t)pos[i] ^ POS_BIAS, row[i] + 1);
   if ((r = upload(&c->d_pr0, pr.data(), pr.size(), c->stream))) return r;
   if ((r = upload(&c->d_pr, pr.data(), pr.size(), c->stream))) return r;
+  c->n_snps = n_snps;
+  // row-sorted blocks: fewer cache lines per coefficient gather, but measured slower once the
+  // coefficient windows follow the walks (the texture data path is bound by bytes, not
+  // lines); kept as an option (FSCLG_SORTED=1), parity-tested
+  if (c->n_rows > 0 && c->n_rows + 1 < 0x10000 && getenv("FSCLG_SORTED")) {
+    sort_blocks(c, pr.data());
+    if ((r = upload(&c->d_prs0, c->h_prs.data(), c->h_prs.size(), c->stream))) return r;
+    if ((r = upload(&c->d_prs, c->h_prs.data(), c->h_prs.size(), c->stream))) return r;
+  } else {
+    if (c->d_prs) hipFree(c->d_prs);
+    if (c->d_prs0) hipFree(c->d_prs0);
+    c->d_prs = nullptr; c->d_prs0 = nullptr;
+  }
   if ((r = upload(&c->d_chr_start, chr_start, (size_t)n_chr, c->stream))) return r;
   if ((r = upload(&c->d_chr_n, chr_n, (size_t)n_chr, c->stream))) return r;
   if ((r = upload<double>(&c->d_chr_null, nullptr, (size_t)n_chr, c->stream))) return r;
@@ -1017,6 +1226,13 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   c->h_chr_start.assign(chr_start, chr_start + n_chr);
   c->h_pos.assign(pos, pos + n_snps);
   c->cell_cost.clear();
+  {  // |d| of a walk stays within a chromosome's span (plus grid slack): branch-2 index range
+    long long span = 0;
+    for (int i = 0; i < n_chr; i++)
+      span = std::max(span, (long long)pos[chr_start[i] + chr_n[i] - 1] - (long long)pos[chr_start[i]]);
+    c->lt_hi = getenv("FSCLG_NO_LTLDS") ? 0 : (int)std::min(32768ll, std::max(256ll, (span >> 16) + 64));
+    if (c->lt_hi <= 256) c->lt_hi = 0;
+  }
   c->h_row_cnt.clear();
   for (int i = 0; i < n_snps; i++) {
     if (pr[i].y >= c->h_row_cnt.size()) c->h_row_cnt.resize(pr[i].y + 1, 0);
@@ -1031,8 +1247,12 @@ int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
   if (!c || !c->d_pr) return set_err(FSCLG_E_STATE, "snps not uploaded");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   c->win_valid = false;
-  if (!row) HIPCHK(hipMemcpyAsync(c->d_pr, c->d_pr0, sizeof(uint2) * c->n_snps, hipMemcpyDeviceToDevice, c->stream), "copy rows");
-  else {
+  if (!row) {
+    HIPCHK(hipMemcpyAsync(c->d_pr, c->d_pr0, sizeof(uint2) * c->n_snps, hipMemcpyDeviceToDevice, c->stream), "copy rows");
+    if (c->d_prs)
+      HIPCHK(hipMemcpyAsync(c->d_prs, c->d_prs0, sizeof(uint2) * c->h_prs.size(), hipMemcpyDeviceToDevice, c->stream),
+             "copy sorted rows");
+  } else {
     c->h_stage.resize(c->n_snps);
     for (int i = 0; i < c->n_snps; i++) {
       if (row[i] >= (uint32_t)c->n_rows) return set_err(FSCLG_E_ARG, "row index out of table");
@@ -1040,7 +1260,12 @@ int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
     }
     HIPCHK(hipMemcpyAsync(c->d_pr, c->h_stage.data(), sizeof(uint2) * c->n_snps, hipMemcpyHostToDevice, c->stream),
            "copy rows");
-    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");  // h_stage is reused
+    if (c->d_prs) {
+      sort_blocks(c, c->h_stage.data());
+      HIPCHK(hipMemcpyAsync(c->d_prs, c->h_prs.data(), sizeof(uint2) * c->h_prs.size(), hipMemcpyHostToDevice, c->stream),
+             "copy sorted rows");
+    }
+    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");  // h_stage and h_prs are reused
   }
   return FSCLG_OK;
 }
@@ -1130,7 +1355,7 @@ static int ensure_windows(fsclg_ctx* c, int er) {
 static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
   c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
-  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8;
+  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0);
   const int K = room < 0 ? 0 : std::min(c->n_iv, room / ((c->n_rows + 1) * 32));
   double htot = 0.0;
   for (double h : hist) htot += h;
@@ -1153,7 +1378,7 @@ static void plan_cache(fsclg_ctx* c) {
   c->plan_dirty = false;
   c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
-  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8;
+  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0);
   if (room < 32 || c->n_iv <= 0 || c->h_pos.empty() || c->h_coarse.empty() || c->h_lt3.empty()) return;
   std::vector<double> hist(c->n_iv, 0.0);
   std::vector<double> las(c->h_coarse);
@@ -1185,7 +1410,7 @@ static void plan_cache(fsclg_ctx* c) {
 
 static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
   Params P;
-  P.pr = c->d_pr; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
+  P.pr = c->d_pr; P.prs = c->d_prs; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
   P.thr = c->d_thr; P.n_rows = c->n_rows; P.stride = c->n_rows + 1;
   P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step - 1e-9;
   // dynamic LDS: the planned coefficient window, thresholds and null rows
@@ -1193,6 +1418,7 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
   P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; P.civ_max = std::max(c->c_civ - 1, 0);
   P.n_cache = P.n_civ * P.stride;
   P.off_b = P.n_cache * 16; P.off_thr = 2 * P.off_b; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
+  P.off_lt = P.off_nul + (c->n_rows + 1) * 8; P.lt_hi = c->lt_hi;
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null; P.win_null = c->d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
@@ -1200,7 +1426,7 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
     if (c->ctrace_cap < n) {
       if (c->d_ctrace) hipFree(c->d_ctrace);
       c->d_ctrace = nullptr;
-      if (hipMalloc((void**)&c->d_ctrace, sizeof(unsigned long long) * 4 * n) == hipSuccess) c->ctrace_cap = n;
+      if (hipMalloc((void**)&c->d_ctrace, sizeof(unsigned long long) * 8 * n) == hipSuccess) c->ctrace_cap = n;
     }
     P.ctrace = c->d_ctrace;
   }
@@ -1212,7 +1438,7 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
 static int launch(fsclg_ctx* c, const Params& P, int n) {
   HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
   const int grid = (n + 7) / 8 * 8;
-  const int dyn = P.off_nul + (P.n_rows + 1) * 8;
+  const int dyn = P.off_lt + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   if (stat + dyn <= LDS_WG) {
     static bool attr = false;
@@ -1269,21 +1495,25 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
          "copy cells");
   Params P = make_params(c, n_cells, 0, eval_range, bp_resl);
   if (c->hist_pending && P.n_civ > 0) {
-    if (c->ivhist_n < c->n_iv) {
+    const int nh = (c->n_coarse + 2) * c->n_iv;  // per phase key
+    if (c->ivhist_n < nh) {
       if (c->d_ivhist) hipFree(c->d_ivhist);
       c->d_ivhist = nullptr; c->ivhist_n = 0;
-      HIPCHK(hipMalloc((void**)&c->d_ivhist, sizeof(unsigned long long) * c->n_iv), "hipMalloc ivhist");
-      c->ivhist_n = c->n_iv;
+      HIPCHK(hipMalloc((void**)&c->d_ivhist, sizeof(unsigned long long) * nh), "hipMalloc ivhist");
+      c->ivhist_n = nh;
     }
-    HIPCHK(hipMemsetAsync(c->d_ivhist, 0, sizeof(unsigned long long) * c->n_iv, c->stream), "hipMemset ivhist");
+    HIPCHK(hipMemsetAsync(c->d_ivhist, 0, sizeof(unsigned long long) * nh, c->stream), "hipMemset ivhist");
     P.ivhist = c->d_ivhist;
   }
   if ((r = launch(c, P, n_cells))) return r;
   if (P.ivhist) {  // re-plan the LDS window from the measured histogram
-    std::vector<unsigned long long> h(c->n_iv);
-    HIPCHK(hipMemcpyAsync(h.data(), P.ivhist, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream),
+    const int nkey = c->n_coarse + 2;
+    std::vector<unsigned long long> hk((size_t)nkey * c->n_iv), h(c->n_iv, 0);
+    HIPCHK(hipMemcpyAsync(hk.data(), P.ivhist, sizeof(unsigned long long) * hk.size(), hipMemcpyDeviceToHost, c->stream),
            "copy ivhist");
     HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    for (int k = 0; k < nkey; k++)
+      for (int j = 0; j < c->n_iv; j++) h[j] += hk[(size_t)k * c->n_iv + j];
     choose_window(c, std::vector<double>(h.begin(), h.end()));
     c->hist_pending = false;
     if (getenv("FSCLG_DEBUG_PLAN")) {  // development aid: coverage of the best window by size
@@ -1299,6 +1529,17 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
         }
         fprintf(stderr, "  K=%3d covers %.3f\n", K, best / tot);
       }
+      for (int k = 0; k < nkey; k++) {  // per phase key: weight, best-window coverage at the planned K
+        double kt = 0, best = 0, run = 0;
+        for (int j = 0; j < c->n_iv; j++) kt += (double)hk[(size_t)k * c->n_iv + j];
+        if (kt <= 0) continue;
+        for (int j = 0; j < c->n_iv; j++) {
+          run += (double)hk[(size_t)k * c->n_iv + j];
+          if (j >= c->c_civ) run -= (double)hk[(size_t)k * c->n_iv + j - c->c_civ];
+          best = std::max(best, run);
+        }
+        fprintf(stderr, "  key %2d: weight %.3f, own best window covers %.3f\n", k, kt / tot, best / kt);
+      }
       for (int j = 0; j < c->n_iv; j += 10) {
         double sub = 0;
         for (int k = j; k < std::min(j + 10, c->n_iv); k++) sub += (double)h[k];
@@ -1306,8 +1547,8 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
       }
     }
   }
-  if (P.ctrace) {  // development aid: append [n, then n x (start, end, cu, terms)] to the file
-    std::vector<unsigned long long> h((size_t)4 * n_cells);
+  if (P.ctrace) {  // development aid: append [n, then n x (start, end, cu, terms, 4 phase times)] to the file
+    std::vector<unsigned long long> h((size_t)8 * n_cells);
     HIPCHK(hipMemcpyAsync(h.data(), P.ctrace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream),
            "copy trace");
     HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
