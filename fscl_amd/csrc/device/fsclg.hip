@@ -43,8 +43,14 @@
 
 namespace {
 
+// 12 waves per workgroup, two workgroups per CU (80 KB LDS each), 6 waves per SIMD: the
+// term loop is latency-bound, and occupancy is what hides it (measured: 3 waves/SIMD 25.5
+// ms, 4 waves 16.2 ms, 6 waves 15.2 ms per C2 launch)
 #ifndef FSCLG_WG
-#define FSCLG_WG 512
+#define FSCLG_WG 768
+#endif
+#ifndef FSCLG_WPE
+#define FSCLG_WPE 6
 #endif
 #ifndef FSCLG_LDS_WG
 #define FSCLG_LDS_WG 81920
@@ -62,7 +68,7 @@ constexpr int MAXTIES = 512;       // per eval_walks; overflow sends the affecte
 constexpr int MAXREF = 16;
 constexpr int LDS_WG = FSCLG_LDS_WG;  // LDS per workgroup (default: two workgroups per CU, 160 KiB)
 #ifndef FSCLG_U
-#define FSCLG_U 4
+#define FSCLG_U 2
 #endif
 constexpr int U = FSCLG_U;         // terms per lane per loop trip (independent load chains)
 constexpr double LOG_AD_MIN = -20.0;  // fscl.h:79
@@ -465,13 +471,30 @@ __device__ __forceinline__ void run_segment(Smem& S, int w, int s, const Params&
   const uint2* src = SORTED ? P.prs : P.pr;
   const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
   double sum = 0.0, mag = 0.0;
+#ifdef FSCLG_PREFETCH  // (position, row) of the next trip loaded one trip ahead (PAD covers the overshoot)
+  uint2 nx[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) nx[u] = ld_pr(src, base + (uint32_t)(64 * u + lane));
+#endif
   for (int kb = 0; kb < n; kb += 64 * U) {
     uint32_t pv[U], rv[U];
     int orig[U];
+#ifdef FSCLG_PREFETCH
+    uint2 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      cur[u] = nx[u];
+      nx[u] = ld_pr(src, base + (uint32_t)(kb + 64 * U + 64 * u + lane));
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int k = kb + 64 * u + lane;
+#ifdef FSCLG_PREFETCH
+      const uint2 v = cur[u];
+#else
       const uint2 v = ld_pr(src, base + (uint32_t)k);
+#endif
       pv[u] = v.x;
       if constexpr (SORTED) {
         orig[u] = (int)base + (int)(v.y >> 16);
@@ -858,7 +881,12 @@ __device__ __forceinline__ void write_point(fsclg_point_t& o, const Pt& pt) {
 }
 
 template <bool LDS>
-__global__ void __launch_bounds__(WG) search_maxpos_kernel(Params P) {
+#ifdef FSCLG_WPE  // waves per SIMD to budget registers for (caps VGPRs at 512 / FSCLG_WPE)
+#define FSCLG_KATTR __attribute__((amdgpu_waves_per_eu(FSCLG_WPE, FSCLG_WPE)))
+#else
+#define FSCLG_KATTR
+#endif
+__global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P) {
   __shared__ Smem S;
   const int tid = threadIdx.x;
   // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous run of cells
