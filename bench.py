@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--genome-scale", type=int, default=1,
+                    help="development: chromosomes per rank (>1 rehearses the host load of a larger job on one GPU)")
     ap.add_argument("--traffic-summary", default=None,
                     help="rocprofv3 PMC summary (tools/prof_summary.py) for roofline.traffic; default: newest in profiles/")
     return ap.parse_args()
@@ -92,7 +94,7 @@ def main() -> int:
     wd.mkdir(parents=True, exist_ok=True)
     snp = wd / f"{args.config}_x{world}_r{rank}.snp"
     gen = dict(cfg)
-    gen["n_chr"] = cfg["n_chr"] * world  # weak scaling: N x the single-GPU genome
+    gen["n_chr"] = cfg["n_chr"] * world * args.genome_scale  # weak scaling: N x the single-GPU genome
     synth.write_snp_file(str(snp), synth.generate(seed=args.seed, sweeps_per_chr=2, **gen))
 
     # ---- untimed setup (input and tables reported separately)
@@ -170,9 +172,9 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded neutral-spectrum SNPs with planted sweeps, fscl_amd/synth.py)",
-        "config": {"workload": f"{args.config}: {world} x ({cfg['snps_per_chr']} SNPs, {cfg['chr_len'] // 10**6} Mb, "
+        "config": {"workload": f"{args.config}: {world * args.genome_scale} x ({cfg['snps_per_chr']} SNPs, {cfg['chr_len'] // 10**6} Mb, "
                                f"n={cfg['n']}) chromosome(s), G=100kb, {n_permute} permutations, parity mode",
-                   "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"] * world,
+                   "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"] * world * args.genome_scale,
                    "units_per_step": units / args.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -184,7 +186,8 @@ def main() -> int:
         "setup_s": setup_s,
         "stats": {k: st[k] for k in ("n_terms", "n_null", "n_walks", "n_unsafe", "n_slow", "n_ties", "trials",
                                      "host_perm_s", "scan_s", "permute_s", "gp_evals",
-                                     "cache_iv0", "cache_n_iv", "cache_n_rows", "cache_cover", "window_ms")},
+                                     "cache_iv0", "cache_n_iv", "cache_n_rows", "cache_cover", "window_ms",
+                                     "host_null_s", "host_upload_s", "search_s", "prune_s")},
     }
 
     # ---- CPU baseline: the oracle port on the host cores, bounded sample = the initial scan

@@ -76,7 +76,8 @@ class Stats(C.Structure):  # fscl_amd_stats_t
                 ("n_unsafe", C.c_ulonglong), ("n_slow", C.c_ulonglong), ("n_ties", C.c_ulonglong),
                 ("n_launches", C.c_ulonglong), ("negj", C.c_ulonglong), ("trials", C.c_int),
                 ("cache_iv0", C.c_int), ("cache_n_iv", C.c_int), ("cache_n_rows", C.c_int),
-                ("cache_cover", C.c_double), ("window_ms", C.c_double)]
+                ("cache_cover", C.c_double), ("window_ms", C.c_double), ("host_null_s", C.c_double),
+                ("host_upload_s", C.c_double), ("search_s", C.c_double), ("prune_s", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1013,6 +1013,13 @@ __global__ void __launch_bounds__(WN_WG) window_null_kernel(const uint2* __restr
   if (nwin > 3) out[base + 3] = a3;
 }
 
+// one trial's rows into the (position, row) array: pr[i].y = row[i] + 1 (device row)
+__global__ void __launch_bounds__(256) scatter_rows_kernel(uint2* __restrict__ pr, const uint32_t* __restrict__ row,
+                                                           int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) pr[i].y = row[i] + 1u;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------- host shim
@@ -1051,6 +1058,9 @@ struct fsclg_ctx {
   std::vector<long long> h_row_cnt;     // sites per device row
   std::vector<double> h_lt3;
   std::vector<uint2> h_stage;
+  uint32_t* h_rows = nullptr;     // pinned staging of one trial's rows
+  uint32_t* d_rows = nullptr;
+  int rows_cap = 0;
   // LDS coefficient cache plan (fsclg_plan_cache)
   bool plan_dirty = true;
   bool hist_pending = false;          // the next search_maxpos launch measures the interval histogram
@@ -1171,6 +1181,8 @@ int fsclg_close(fsclg_ctx* c) {
   void* ptrs[] = {c->d_ctrace, c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr, c->d_pr0, c->d_prs, c->d_prs0, c->d_chr_start, c->d_chr_n,
                   c->d_chr_null, c->d_win_null, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
+  if (c->d_rows) hipFree(c->d_rows);
+  if (c->h_rows) hipHostFree(c->h_rows);
   hipEventDestroy(c->ev0);
   hipEventDestroy(c->ev1);
   hipStreamDestroy(c->stream);
@@ -1271,6 +1283,23 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   return FSCLG_OK;
 }
 
+static int ensure_row_staging(fsclg_ctx* c) {
+  if (c->rows_cap >= c->n_snps) return FSCLG_OK;
+  if (c->h_rows) hipHostFree(c->h_rows);
+  if (c->d_rows) hipFree(c->d_rows);
+  c->h_rows = nullptr; c->d_rows = nullptr; c->rows_cap = 0;
+  HIPCHK(hipHostMalloc((void**)&c->h_rows, sizeof(uint32_t) * c->n_snps, hipHostMallocDefault), "hipHostMalloc rows");
+  HIPCHK(hipMalloc((void**)&c->d_rows, sizeof(uint32_t) * c->n_snps), "hipMalloc rows");
+  c->rows_cap = c->n_snps;
+  return FSCLG_OK;
+}
+
+uint32_t* fsclg_row_buffer(fsclg_ctx* c) {
+  if (!c || !c->d_pr) { set_err(FSCLG_E_STATE, "snps not uploaded"); return nullptr; }
+  if (hipSetDevice(c->device) != hipSuccess || ensure_row_staging(c) != FSCLG_OK) return nullptr;
+  return c->h_rows;
+}
+
 int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
   if (!c || !c->d_pr) return set_err(FSCLG_E_STATE, "snps not uploaded");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
@@ -1281,19 +1310,26 @@ int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
       HIPCHK(hipMemcpyAsync(c->d_prs, c->d_prs0, sizeof(uint2) * c->h_prs.size(), hipMemcpyDeviceToDevice, c->stream),
              "copy sorted rows");
   } else {
-    c->h_stage.resize(c->n_snps);
-    for (int i = 0; i < c->n_snps; i++) {
-      if (row[i] >= (uint32_t)c->n_rows) return set_err(FSCLG_E_ARG, "row index out of table");
-      c->h_stage[i] = make_uint2(c->h_pr0[i].x, row[i] + 1);
-    }
-    HIPCHK(hipMemcpyAsync(c->d_pr, c->h_stage.data(), sizeof(uint2) * c->n_snps, hipMemcpyHostToDevice, c->stream),
+    uint32_t mx = 0;
+    for (int i = 0; i < c->n_snps; i++) mx = row[i] > mx ? row[i] : mx;  // vectorised validation
+    if (mx >= (uint32_t)c->n_rows) return set_err(FSCLG_E_ARG, "row index out of table");
+    int r;
+    if ((r = ensure_row_staging(c))) return r;
+    // the previous trial's copy has completed (its search synchronised the stream)
+    if (row != c->h_rows) memcpy(c->h_rows, row, sizeof(uint32_t) * c->n_snps);
+    HIPCHK(hipMemcpyAsync(c->d_rows, c->h_rows, sizeof(uint32_t) * c->n_snps, hipMemcpyHostToDevice, c->stream),
            "copy rows");
-    if (c->d_prs) {
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3((c->n_snps + 255) / 256), dim3(256), 0, c->stream, c->d_pr,
+                       c->d_rows, c->n_snps);
+    HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
+    if (c->d_prs) {  // opt-in row-sorted blocks: built on the host
+      c->h_stage.resize(c->n_snps);
+      for (int i = 0; i < c->n_snps; i++) c->h_stage[i] = make_uint2(c->h_pr0[i].x, row[i] + 1);
       sort_blocks(c, c->h_stage.data());
       HIPCHK(hipMemcpyAsync(c->d_prs, c->h_prs.data(), sizeof(uint2) * c->h_prs.size(), hipMemcpyHostToDevice, c->stream),
              "copy sorted rows");
+      HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");  // h_prs is reused
     }
-    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");  // h_stage and h_prs are reused
   }
   return FSCLG_OK;
 }

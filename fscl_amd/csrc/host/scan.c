@@ -295,6 +295,7 @@ static void prepare(scan_t *s, sm_ptable_t *sm) {
    over the whole chromosome for the given rows */
 static void chr_null_sums(const uint32_t *row, double *out) {
   int c, i;
+#pragma omp parallel for schedule(dynamic, 1) private(i) if (D.n_chr > 1)
   for (c = 0; c < D.n_chr; c++) {
     double acc = 0.;
     for (i = D.chr_start[c]; i < D.chr_start[c] + D.chr_n[c]; i++) acc += D.nullrow[row[i]];
@@ -430,13 +431,43 @@ static void block_permute(uint32_t *prow, const uint32_t *row, const snp_t *snps
     j = r1 / (2147483647 + 1.0) * n;
     if (r2 == 0) k = n; /* Q10: log(0) */
     else k = j + (int)(-1.0 / nbp * log(r2 / (2147483647 + 1.0)));
-    while (k < n && snps[k].chr == snps[j].chr && snps[k].pos - snps[j].pos < width) k++;
+    /* scan-chromosome.c:355-357: extend k while on j's chromosome and within width of
+       pos[j]; positions ascend within a chromosome, so the stop is a lower bound */
+    if (k >= 0 && k < n && snps[k].chr == snps[j].chr) {
+      const int c = snps[j].chr, ce = D.chr_start[c] + D.chr_n[c];
+      const int32_t pj = D.pos[j];
+      int lo = k, hi = ce, step = 1; /* first index in [k, ce) with pos - pj >= width, else ce */
+      while (lo + step < ce && (double)(D.pos[lo + step] - pj) < width) { lo += step; step <<= 1; } /* gallop */
+      if (lo + step < ce) hi = lo + step;
+      if ((double)(D.pos[lo] - pj) < width) lo++; /* lo itself is inside (or is k, unchecked) */
+      while (lo < hi) {
+        const int m = lo + (hi - lo) / 2;
+        if ((double)(D.pos[m] - pj) < width) lo = m + 1; else hi = m;
+      }
+      k = lo;
+    }
     if (i + (k - j) >= n) k = n;
     if (k > n) { D.st.negj++; j -= k - n; k = n; }
-    for (; j < k && i < n && j < n; i++, j++) {
-      const uint32_t t = prow[i];
-      prow[i] = prow[j];
-      prow[j] = t;
+    {
+      /* scan-chromosome.c:365-372: swap p[i++] with p[j++] while j < k and i < n; disjoint
+         ranges in one vectorisable pass, overlapping ones element by element as written */
+      const int len = (k - j < n - i) ? k - j : n - i;
+      if (len > 0 && (j >= i + len || i >= j + len)) {
+        uint32_t *__restrict a = prow + i, *__restrict b = prow + j;
+        int t;
+        for (t = 0; t < len; t++) {
+          const uint32_t x = a[t];
+          a[t] = b[t];
+          b[t] = x;
+        }
+        i += len;
+        j += len;
+      }
+      for (; j < k && i < n && j < n; i++, j++) {
+        const uint32_t t = prow[i];
+        prow[i] = prow[j];
+        prow[j] = t;
+      }
     }
   }
 }
@@ -477,7 +508,9 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   sigaction(SIGINT, &sa, NULL);
   fh_srand(&g, PERM_SEED);
   (void)fh_rand(&g); /* scan-chromosome.c:440: the single thread's usleep() draw */
-  prow = fh_malloc(sizeof(uint32_t) * s->n_snps, "permuted rows");
+  /* the permutation is written straight into the device context's pinned staging */
+  prow = fsclg_row_buffer(D.ctx);
+  if (!prow) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
   act = fh_malloc(sizeof(int) * (n_act ? n_act : 1), "active points");
   cells = fh_malloc(sizeof(fsclg_cell_t) * (n_act ? n_act : 1), "cells");
   out = fh_malloc(sizeof(fsclg_point_t) * (n_act ? n_act : 1), "points");
@@ -496,9 +529,13 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
     n_act = k;
     cr_logmsg(MSG_STATUS, "Scanning snp block permutations... %7d (%d scan pts remaining)        ", trial, n_act);
     if (n_act == 0 || trial > n_perm) break;
+    tp = fh_now();
     chr_null_sums(prow, nul);
+    D.st.host_null_s += fh_now() - tp;
+    tp = fh_now();
     dev_check(fsclg_set_rows(D.ctx, prow), "set rows");
     dev_check(fsclg_set_chr_null(D.ctx, nul), "set null sums");
+    D.st.host_upload_s += fh_now() - tp;
     for (i = 0; i < n_act; i++) {
       const scan_pt_t *q = s->scan_pts + act[i];
       cells[i].chr = q->chr;
@@ -506,7 +543,10 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
       cells[i].end_pos = cells[i].start_pos + large_grid_sp;
       cells[i].pad = 0;
     }
+    tp = fh_now();
     eval_cells(cells, n_act, eval_range, bp_resl, out);
+    D.st.search_s += fh_now() - tp;
+    tp = fh_now();
     D.st.trials++;
     for (i = 0; i < n_act; i++) { /* scan-chromosome.c:488-502, ascending point order */
       scan_pt_t *q = s->scan_pts + act[i];
@@ -521,6 +561,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
       if (clr < 0 || clr > 1000000 || isnan(clr))
         fprintf(stderr, "%d\t%d\t%g\t%1.3e\n", q->chr, cells[i].start_pos, clr, exp(out[i].lalpha));
     }
+    D.st.prune_s += fh_now() - tp;
     if (g_sigint && D.rank == 0) {
       g_sigint = 0;
       scan_output(output_fname, s, 0, n_permute, prepend_label);
@@ -531,7 +572,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   cr_logmsg(MSG_STATUS, "Scanning snp block permutations... finished.\n");
   signal(SIGINT, SIG_DFL);
   dev_check(fsclg_set_rows(D.ctx, NULL), "set rows");
-  free(prow); free(act); free(cells); free(out); free(nul);
+  free(act); free(cells); free(out); free(nul);
   D.st.permute_s += fh_now() - t0;
 }
 

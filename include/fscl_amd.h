@@ -169,6 +169,10 @@ typedef struct {
   int cache_iv0, cache_n_iv, cache_n_rows;  /* LDS coefficient window (fsclg_stats_t) */
   double cache_cover;
   double window_ms;       /* window null-sum kernels (chromosomes above 2*eval_range+1 SNPs) */
+  double host_null_s;     /* scan_permute host phases: per-chromosome null sums */
+  double host_upload_s;   /*   rows + null sums to the device */
+  double search_s;        /*   cell evaluation (launch, kernel, results, rank exchange) */
+  double prune_s;         /*   pruning and bookkeeping */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

@@ -86,6 +86,10 @@ int fsclg_upload_snps(fsclg_ctx *c, const int32_t *pos, const uint32_t *row, int
                       const int32_t *chr_start, const int32_t *chr_n, int n_chr);
 
 /* replace the per-site rows (one permutation trial); NULL restores the uploaded rows */
+/* a pinned host buffer of n_snps rows owned by the context (valid until the next
+   fsclg_upload_snps / fsclg_close): a caller that permutes into it saves one copy in
+   fsclg_set_rows (the buffer may be rewritten once fsclg_set_rows's search has returned) */
+uint32_t *fsclg_row_buffer(fsclg_ctx *c);
 int fsclg_set_rows(fsclg_ctx *c, const uint32_t *row);
 
 /* sequential window null sums (init_scan_result's sum from 0.0) for each chromosome's
