@@ -111,7 +111,7 @@ struct Params {
   int ivc0;                    // LDS coefficient cache: intervals [ivc0, ivc0 + n_civ), every row
   int n_civ, civ_max;          // civ_max = max(n_civ - 1, 0)
   int n_cache;                 // n_civ * stride blocks
-  int off_b, off_thr, off_nul; // byte offsets in fsclg_dyn (plane A at 0)
+  int off_thr, off_nul;        // byte offsets in fsclg_dyn (the coefficient window at 0)
   int off_lt, lt_hi;           // LDS copy of logt3 branch 2 (|d| > 2^24) entries [256, lt_hi) at off_lt; lt_hi 0: none
   int eval_range;
   int bp_resl;
@@ -191,7 +191,7 @@ __device__ __forceinline__ double logt_lds(uint32_t ad, const Params& P) {
   if constexpr (LDS) {
     const uint32_t i2 = ad >> 16;
     if (ad > 0xFFFFFFu && i2 < (uint32_t)P.lt_hi)
-      return reinterpret_cast<const double*>(fsclg_dyn + P.off_lt)[i2 - 256u];
+      return reinterpret_cast<const double*>(fsclg_dyn + P.off_lt)[i2];  // off_lt is pre-offset by -256 entries
   }
   return logt_dev(ad, P.logt3);
 }
@@ -213,8 +213,10 @@ __device__ __forceinline__ double log_ad_of(int i, int sweep, double la, const P
 // settles it (thr[n_iv] = +inf: the reference clamps at n_iv - 1)
 template <bool LDS>
 __device__ __forceinline__ int interval_of(double x, const Smem& S, const Params& P) {
+  // x >= LOG_AD_MIN (log_table >= 0 and every alpha >= LOG_AD_MIN, checked by
+  // fsclg_set_alpha_grid), so the estimate is >= -1e-9 and truncates to >= 0
   int iv = (int)__builtin_fma(x, P.inv_step, P.iv_off);
-  iv = min(max(iv, 0), P.n_iv - 1);
+  iv = min(iv, P.n_iv - 1);
   double hi;
   if constexpr (LDS) hi = reinterpret_cast<const double*>(fsclg_dyn + P.off_thr)[iv + 1];
   else hi = P.thr[iv + 1];
@@ -251,8 +253,8 @@ __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, co
     const uint32_t ci = (uint32_t)(iv - S.ivc0);
     const bool hit = ci < (uint32_t)P.n_civ;  // every row is cached
     const uint32_t li = __umul24(min(ci, (uint32_t)P.civ_max), (uint32_t)P.stride) + r;
-    a = reinterpret_cast<const double2*>(fsclg_dyn)[li];
-    b = reinterpret_cast<const double2*>(fsclg_dyn + P.off_b)[li];
+    a = reinterpret_cast<const double2*>(fsclg_dyn)[2 * li];
+    b = reinterpret_cast<const double2*>(fsclg_dyn)[2 * li + 1];
     if (!hit) {
       const double2* cp = coef_of(r, iv, P);
       a = cp[0];
@@ -283,9 +285,9 @@ __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t 
     for (int u = 0; u < U; u++) {
       const uint32_t ci = (uint32_t)(iv[u] - ivc0);
       if (ci < (uint32_t)P.n_civ) {  // every row is cached
-        const uint32_t li = __umul24(ci, (uint32_t)P.stride) + rv[u];
-        ca[u] = reinterpret_cast<const double2*>(fsclg_dyn)[li];
-        cb[u] = reinterpret_cast<const double2*>(fsclg_dyn + P.off_b)[li];
+        const double2* lp = reinterpret_cast<const double2*>(fsclg_dyn) + 2 * (__umul24(ci, (uint32_t)P.stride) + rv[u]);
+        ca[u] = lp[0];
+        cb[u] = lp[1];
       } else {
         const double2* cp = coef_of(rv[u], iv[u], P);
         ca[u] = cp[0];
@@ -513,8 +515,10 @@ __device__ __forceinline__ void run_segment(Smem& S, int w, int s, const Params&
       x[u] = logt_lds<LDS>(absdist(pv[u], usweep), P) + la;
 #endif
     }
-    if (P.ivhist && kb == 0 && lane == 0)  // one sample per segment, weighted by its terms
+#ifdef FSCLG_IVHIST  // diagnostic: one interval sample per segment, weighted by its terms
+    if (P.ivhist && kb == 0 && lane == 0)
       atomicAdd(&P.ivhist[S.hkey * P.n_iv + interval_of<LDS>(x[0], S, P)], (unsigned long long)(ie - ib));
+#endif
     double2 ca[U], cb[U];
     coef_stage<LDS>(x, rv, S, P, ivc0, ca, cb);
 #pragma unroll
@@ -650,17 +654,13 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
 }
 
 // evaluate S.nwalk walks (already holding p, la) -> exact values in S.val
-// stage the coefficient blocks of intervals [wb, wb + n_civ) x every row into the LDS
-// planes (all threads; the caller brackets it with barriers)
+// stage the coefficient blocks of intervals [wb, wb + n_civ) x every row into LDS, in the
+// table's own [iv][row][4] layout: one contiguous copy (all threads; the caller brackets
+// it with barriers)
 __device__ __forceinline__ void load_window(Smem& S, const Params& P, int wb) {
-  double2* ca = reinterpret_cast<double2*>(fsclg_dyn);
-  double2* cb = reinterpret_cast<double2*>(fsclg_dyn + P.off_b);
+  double2* dst = reinterpret_cast<double2*>(fsclg_dyn);
   const double2* src = reinterpret_cast<const double2*>(P.coef) + (size_t)wb * P.stride * 2;
-  for (int e = threadIdx.x; e < P.n_cache; e += WG) {  // the window is one contiguous run of [iv][row] blocks
-    const double2 a = src[2 * e], b = src[2 * e + 1];
-    ca[e] = a;
-    cb[e] = b;
-  }
+  for (int e = threadIdx.x; e < 2 * P.n_cache; e += WG) dst[e] = src[e];
   if (threadIdx.x == 0) S.ivc0 = wb;
 }
 
@@ -755,17 +755,22 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
         if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
         cw = w; acc = 0.0; accm = 0.0;
       }
+#ifdef FSCLG_SORTED_PATH
       if (S.w[w].srt) run_segment<LDS, true>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
-      else run_segment<LDS, false>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+      else
+#endif
+      run_segment<LDS, false>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
      }
     }
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
   }
   __syncthreads();
+#ifdef FSCLG_SORTED_PATH
   if (P.prs) {
     fix_ties<LDS>(S, P, wave, lane);
     __syncthreads();
   }
+#endif
   PHASE_MARK(2);
   TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk(S, tid);
@@ -900,14 +905,11 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
   if constexpr (LDS) {
     double* thr = reinterpret_cast<double*>(fsclg_dyn + P.off_thr);
     double* nul = reinterpret_cast<double*>(fsclg_dyn + P.off_nul);
-    double2* ca = reinterpret_cast<double2*>(fsclg_dyn);
-    double2* cb = reinterpret_cast<double2*>(fsclg_dyn + P.off_b);
     for (int j = tid; j <= P.n_iv; j += WG) thr[j] = P.thr[j];
     for (int j = tid; j <= P.n_rows; j += WG) nul[j] = P.nullrow[j];  // + sentinel
-    (void)ca; (void)cb;
     load_window(S, P, P.ivc0);
     double* lt2 = reinterpret_cast<double*>(fsclg_dyn + P.off_lt);
-    for (int j = tid; j < P.lt_hi - 256; j += WG) lt2[j] = P.logt3[2 * 0x10000 + 256 + j];
+    for (int j = 256 + tid; j < P.lt_hi; j += WG) lt2[j] = P.logt3[2 * 0x10000 + j];
   } else if (tid == 0) S.ivc0 = 0;
   __syncthreads();
   if (P.mode == 1) {
@@ -1247,7 +1249,12 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   // row-sorted blocks: fewer cache lines per coefficient gather, but measured slower once the
   // coefficient windows follow the walks (the texture data path is bound by bytes, not
   // lines); kept as an option (FSCLG_SORTED=1), parity-tested
-  if (c->n_rows > 0 && c->n_rows + 1 < 0x10000 && getenv("FSCLG_SORTED")) {
+#ifdef FSCLG_SORTED_PATH
+  const bool sorted_path = true;
+#else
+  const bool sorted_path = false;
+#endif
+  if (sorted_path && c->n_rows > 0 && c->n_rows + 1 < 0x10000 && getenv("FSCLG_SORTED")) {
     sort_blocks(c, pr.data());
     if ((r = upload(&c->d_prs0, c->h_prs.data(), c->h_prs.size(), c->stream))) return r;
     if ((r = upload(&c->d_prs, c->h_prs.data(), c->h_prs.size(), c->stream))) return r;
@@ -1345,6 +1352,11 @@ int fsclg_set_alpha_grid(fsclg_ctx* c, const double* coarse, int n_coarse, const
   if (!c || !coarse || !refine || !n_refine || n_coarse <= 0 || n_coarse * 2 > MAXWALK) return set_err(FSCLG_E_ARG, "alpha grid");
   for (int i = 0; i <= n_coarse; i++)
     if (n_refine[i] < 0 || n_refine[i] > MAXREF) return set_err(FSCLG_E_ARG, "refine count");
+  for (int i = 0; i < n_coarse; i++)  // interval_of relies on x = log(d) + alpha >= LOG_AD_MIN
+    if (!(coarse[i] >= LOG_AD_MIN)) return set_err(FSCLG_E_ARG, "alpha below LOG_AD_MIN");
+  for (int i = 0; i <= n_coarse; i++)
+    for (int r = 0; r < n_refine[i]; r++)
+      if (!(refine[i * MAXREF + r] >= LOG_AD_MIN)) return set_err(FSCLG_E_ARG, "alpha below LOG_AD_MIN");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
   if ((r = upload(&c->d_la_coarse, coarse, (size_t)n_coarse, c->stream))) return r;
@@ -1469,7 +1481,9 @@ static void plan_cache(fsclg_ctx* c) {
     }
   }
   choose_window(c, hist);
-  c->hist_pending = true;  // the first launch measures the real histogram (refine grids follow the data)
+#ifdef FSCLG_IVHIST  // diagnostic builds measure the real histogram in the first launch
+  c->hist_pending = true;
+#endif
 }
 
 static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
@@ -1481,8 +1495,8 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
   if (c->plan_dirty) plan_cache(c);
   P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; P.civ_max = std::max(c->c_civ - 1, 0);
   P.n_cache = P.n_civ * P.stride;
-  P.off_b = P.n_cache * 16; P.off_thr = 2 * P.off_b; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
-  P.off_lt = P.off_nul + (c->n_rows + 1) * 8; P.lt_hi = c->lt_hi;
+  P.off_thr = P.n_cache * 32; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
+  P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8; P.lt_hi = c->lt_hi;  // entry i at off_lt + 8 i
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null; P.win_null = c->d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
@@ -1502,7 +1516,7 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
 static int launch(fsclg_ctx* c, const Params& P, int n) {
   HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
   const int grid = (n + 7) / 8 * 8;
-  const int dyn = P.off_lt + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
+  const int dyn = P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   if (stat + dyn <= LDS_WG) {
     static bool attr = false;
