@@ -58,7 +58,7 @@ namespace {
 constexpr int WG = FSCLG_WG;
 constexpr int NWAVE = WG / 64;
 #ifndef FSCLG_SEG
-#define FSCLG_SEG 1024
+#define FSCLG_SEG 2048
 #endif
 constexpr int SEG = FSCLG_SEG;     // terms per work segment
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
