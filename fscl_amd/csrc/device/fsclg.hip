@@ -116,7 +116,12 @@ struct Params {
   int eval_range;
   int bp_resl;
   int n_cells;
-  int mode;                    // 0: search_maxpos on cells, 1: search_maxalpha on given points
+  int mode;                    // 0: search_maxpos on cells, 1: search_maxalpha on given points,
+                               // 2: search_maxalpha on cell endpoints (epos, two per block) into ept
+  const int2* epos;            // mode 2: (chr, position) of each distinct endpoint
+  int n_ep;
+  fsclg_point_t* ept;          // mode 2 out / mode 0 in: evaluated endpoints
+  const int2* cell_ep;         // mode 0: (start, end) endpoint indices of each cell, or null
 };
 
 struct Pt {                     // one scan point being evaluated (scan_pt_t subset)
@@ -879,6 +884,13 @@ __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, in
   }
 }
 
+__device__ __forceinline__ void read_point(Pt& pt, const fsclg_point_t& in) {
+  pt.chr = in.chr; pt.nearest = in.nearest_snp; pt.sweep = in.sweep_pos; pt.n_snps = in.n_snps;
+  pt.wstart = in.window_start; pt.wend = in.window_end; pt.flags = in.flags;
+  pt.la = in.lalpha; pt.N = in.null_logl; pt.sm = in.sm_logl; pt.clr = in.clr;
+  set_binade(pt);
+}
+
 __device__ __forceinline__ void write_point(fsclg_point_t& o, const Pt& pt) {
   o.chr = pt.chr; o.nearest_snp = pt.nearest; o.sweep_pos = pt.sweep; o.n_snps = pt.n_snps;
   o.window_start = pt.wstart; o.window_end = pt.wend; o.flags = pt.flags; o.cost = 0;
@@ -923,12 +935,25 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
     if (tid == 0) S.cnt[1] += (unsigned long long)S.pt[0].n_snps;
     search_maxalpha_pts<LDS>(S, P, 0, 1);
     if (tid == 0) write_point(P.out[cell], S.pt[0]);
+  } else if (P.mode == 2) {
+    // distinct cell endpoints, two per block: scan-chromosome.c:130-134 for each
+    const int e0 = 2 * cell, np = min(2, P.n_ep - e0);
+    if (tid < np) init_point(S.pt[tid], P.epos[e0 + tid].x, P.epos[e0 + tid].y, P);
+    __syncthreads();
+    if (tid == 0) for (int k = 0; k < np; k++) S.cnt[1] += (unsigned long long)S.pt[k].n_snps;
+    search_maxalpha_pts<LDS>(S, P, 0, np);
+    if (tid < np) write_point(P.ept[e0 + tid], S.pt[tid]);
   } else {
     const fsclg_cell_t c = P.cells[cell];
-    if (tid < 2) init_point(S.pt[tid], c.chr, tid == 0 ? c.start_pos : c.end_pos, P);
-    __syncthreads();
-    if (tid == 0) S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps);
-    search_maxalpha_pts<LDS>(S, P, 0, 2);  // start and end points share the two phases
+    if (P.cell_ep) {  // endpoints evaluated by a mode-2 launch (shared with the neighbouring cells)
+      if (tid < 2) read_point(S.pt[tid], P.ept[tid == 0 ? P.cell_ep[cell].x : P.cell_ep[cell].y]);
+      __syncthreads();
+    } else {
+      if (tid < 2) init_point(S.pt[tid], c.chr, tid == 0 ? c.start_pos : c.end_pos, P);
+      __syncthreads();
+      if (tid == 0) S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps);
+      search_maxalpha_pts<LDS>(S, P, 0, 2);  // start and end points share the two phases
+    }
     int iter = 0;
     for (;;) {
       const int sp = S.pt[0].sweep, ep = S.pt[1].sweep;
@@ -1086,6 +1111,16 @@ struct fsclg_ctx {
   std::vector<fsclg_cell_t> h_cells;
   std::vector<int> h_order;
   std::vector<fsclg_point_t> h_out;
+  // cell / endpoint deduplication
+  std::unordered_map<unsigned long long, int> h_umap, h_emap;
+  std::vector<int> h_uidx, h_upos;
+  std::vector<fsclg_cell_t> h_ucells;
+  std::vector<int2> h_epos, h_cell_ep, h_ucell_ep;
+  int2* d_epos = nullptr;
+  int2* d_cell_ep = nullptr;
+  fsclg_point_t* d_ept = nullptr;
+  int epos_cap = 0, cell_ep_cap = 0, ept_cap = 0;
+  unsigned long long n_dup_cells = 0, n_ep_saved = 0;
   unsigned long long* d_ctrace = nullptr;  // FSCLG_CELL_TRACE=<file>: per-cell timing appended per launch
   int ctrace_cap = 0;
   double kernel_ms = 0.0;
@@ -1181,7 +1216,7 @@ int fsclg_close(fsclg_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_ctrace, c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr, c->d_pr0, c->d_prs, c->d_prs0, c->d_chr_start, c->d_chr_n,
-                  c->d_chr_null, c->d_win_null, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
+                  c->d_chr_null, c->d_win_null, c->d_wtasks, c->d_epos, c->d_cell_ep, c->d_ept, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
   if (c->d_rows) hipFree(c->d_rows);
   if (c->h_rows) hipHostFree(c->h_rows);
@@ -1500,6 +1535,7 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null; P.win_null = c->d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
+  P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
   if (getenv("FSCLG_CELL_TRACE")) {
     if (c->ctrace_cap < n) {
       if (c->d_ctrace) hipFree(c->d_ctrace);
@@ -1513,9 +1549,9 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
   return P;
 }
 
-static int launch(fsclg_ctx* c, const Params& P, int n) {
-  HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
-  const int grid = (n + 7) / 8 * 8;
+// one launch of search_maxpos_kernel with n blocks (events recorded by the caller)
+static int launch_blocks(fsclg_ctx* c, const Params& P, int n) {
+  const int grid = n;
   const int dyn = P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   if (stat + dyn <= LDS_WG) {
@@ -1529,8 +1565,28 @@ static int launch(fsclg_ctx* c, const Params& P, int n) {
   } else
     hipLaunchKernelGGL(search_maxpos_kernel<false>, dim3(grid), dim3(WG), 0, c->stream, P);
   HIPCHK(hipGetLastError(), "launch search_maxpos_kernel");
+  return FSCLG_OK;
+}
+
+static int launch(fsclg_ctx* c, const Params& P, int n) {
+  HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
+  int r;
+  if ((r = launch_blocks(c, P, n))) return r;
   HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
   return FSCLG_OK;
+}
+
+extern "C++" {
+template <typename T>
+static int ensure_buf(T** d, int* cap, int n) {
+  if (n <= *cap) return FSCLG_OK;
+  if (*d) hipFree(*d);
+  *d = nullptr; *cap = 0;
+  const int k = n < 1024 ? 1024 : n;
+  HIPCHK(hipMalloc((void**)d, sizeof(T) * k), "hipMalloc");
+  *cap = k;
+  return FSCLG_OK;
+}
 }
 
 int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, int eval_range, int bp_resl,
@@ -1549,41 +1605,90 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
   int r;
   if ((r = ensure_windows(c, eval_range))) return r;
   if ((r = ensure_io(c, n_cells))) return r;
-  // longest first: each cell's cost in its last launch (permutation trials repeat the cells),
-  // else a guess (cells nearer the middle of a chromosome walk further on both sides)
+  // identical cells are evaluated once (permutation cells are G-aligned, so two points can
+  // share one), and so is an endpoint shared by neighbouring cells (scan-chromosome.c:130-134
+  // evaluates both ends of every cell): a first launch evaluates the distinct endpoints, the
+  // cell launch reads them.  Same inputs, same device arithmetic: identical results.
   auto key = [](const fsclg_cell_t& x) {
     return ((unsigned long long)(uint32_t)x.chr << 58) ^ ((unsigned long long)(uint32_t)x.start_pos << 29) ^
            (unsigned long long)(uint32_t)x.end_pos;
   };
-  std::vector<double> cost(n_cells);
+  auto pkey = [](int chr, int pos) { return ((unsigned long long)(uint32_t)chr << 32) | (uint32_t)pos; };
+  c->h_umap.clear();
+  c->h_ucells.clear();
+  c->h_uidx.resize(n_cells);
   for (int i = 0; i < n_cells; i++) {
-    auto it = c->cell_cost.find(key(cells[i]));
-    if (it != c->cell_cost.end()) { cost[i] = it->second; continue; }
-    const int a = c->h_chr_start[cells[i].chr], nn = c->h_chr_n[cells[i].chr];
-    const double lo = c->h_pos[a], hi = c->h_pos[a + nn - 1], span = hi > lo ? hi - lo : 1.0;
-    const double m = std::min(std::max(cells[i].start_pos - lo, 0.0), std::max(hi - cells[i].start_pos, 0.0));
-    cost[i] = 1e-3 * nn * (1.0 + 2.0 * m / span);
+    auto ins = c->h_umap.emplace(key(cells[i]), (int)c->h_ucells.size());
+    if (ins.second) c->h_ucells.push_back(cells[i]);
+    c->h_uidx[i] = ins.first->second;
   }
-  c->h_order.resize(n_cells);
-  for (int i = 0; i < n_cells; i++) c->h_order[i] = i;
-  std::stable_sort(c->h_order.begin(), c->h_order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
-  c->h_cells.resize(n_cells);
-  for (int k = 0; k < n_cells; k++) c->h_cells[k] = cells[c->h_order[k]];
-  HIPCHK(hipMemcpyAsync(c->d_cells, c->h_cells.data(), sizeof(fsclg_cell_t) * n_cells, hipMemcpyHostToDevice, c->stream),
-         "copy cells");
-  Params P = make_params(c, n_cells, 0, eval_range, bp_resl);
-  if (c->hist_pending && P.n_civ > 0) {
-    const int nh = (c->n_coarse + 2) * c->n_iv;  // per phase key
-    if (c->ivhist_n < nh) {
-      if (c->d_ivhist) hipFree(c->d_ivhist);
-      c->d_ivhist = nullptr; c->ivhist_n = 0;
-      HIPCHK(hipMalloc((void**)&c->d_ivhist, sizeof(unsigned long long) * nh), "hipMalloc ivhist");
-      c->ivhist_n = nh;
+  const int nu = (int)c->h_ucells.size();
+  c->n_dup_cells += (unsigned long long)(n_cells - nu);
+  c->h_emap.clear();
+  c->h_epos.clear();
+  c->h_ucell_ep.resize(nu);
+  for (int u = 0; u < nu; u++) {
+    const fsclg_cell_t& x = c->h_ucells[u];
+    int e[2];
+    for (int k = 0; k < 2; k++) {
+      const int pos = k ? x.end_pos : x.start_pos;
+      auto ins = c->h_emap.emplace(pkey(x.chr, pos), (int)c->h_epos.size());
+      if (ins.second) c->h_epos.push_back(make_int2(x.chr, pos));
+      e[k] = ins.first->second;
     }
+    c->h_ucell_ep[u] = make_int2(e[0], e[1]);
+  }
+  const int ne = (int)c->h_epos.size();
+  const bool use_ep = !getenv("FSCLG_NO_DEDUP") && (2 * nu - ne) * 8 >= nu;  // saves >= 1/8 of the endpoint work
+  // longest first: each cell's cost in its last launch (permutation trials repeat the cells),
+  // else a guess (cells nearer the middle of a chromosome walk further on both sides)
+  std::vector<double> cost(nu);
+  for (int u = 0; u < nu; u++) {
+    const fsclg_cell_t& x = c->h_ucells[u];
+    auto it = c->cell_cost.find(key(x));
+    if (it != c->cell_cost.end()) { cost[u] = it->second; continue; }
+    const int a = c->h_chr_start[x.chr], nn = c->h_chr_n[x.chr];
+    const double lo = c->h_pos[a], hi = c->h_pos[a + nn - 1], span = hi > lo ? hi - lo : 1.0;
+    const double m = std::min(std::max(x.start_pos - lo, 0.0), std::max(hi - x.start_pos, 0.0));
+    cost[u] = 1e-3 * nn * (1.0 + 2.0 * m / span);
+  }
+  c->h_order.resize(nu);
+  for (int u = 0; u < nu; u++) c->h_order[u] = u;
+  std::stable_sort(c->h_order.begin(), c->h_order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+  c->h_cells.resize(nu);
+  c->h_cell_ep.resize(nu);
+  c->h_upos.resize(nu);
+  for (int k = 0; k < nu; k++) {
+    c->h_cells[k] = c->h_ucells[c->h_order[k]];
+    c->h_cell_ep[k] = c->h_ucell_ep[c->h_order[k]];
+    c->h_upos[c->h_order[k]] = k;
+  }
+  if ((r = ensure_io(c, nu))) return r;
+  HIPCHK(hipMemcpyAsync(c->d_cells, c->h_cells.data(), sizeof(fsclg_cell_t) * nu, hipMemcpyHostToDevice, c->stream),
+         "copy cells");
+  Params P = make_params(c, nu, 0, eval_range, bp_resl);
+  if (c->hist_pending && P.n_civ > 0) {  // diagnostic builds (FSCLG_IVHIST): per phase key
+    const int nh = (c->n_coarse + 2) * c->n_iv;
+    if ((r = ensure_buf(&c->d_ivhist, &c->ivhist_n, nh))) return r;
     HIPCHK(hipMemsetAsync(c->d_ivhist, 0, sizeof(unsigned long long) * nh, c->stream), "hipMemset ivhist");
     P.ivhist = c->d_ivhist;
   }
-  if ((r = launch(c, P, n_cells))) return r;
+  HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
+  if (use_ep) {
+    if ((r = ensure_buf(&c->d_epos, &c->epos_cap, ne))) return r;
+    if ((r = ensure_buf(&c->d_ept, &c->ept_cap, ne))) return r;
+    if ((r = ensure_buf(&c->d_cell_ep, &c->cell_ep_cap, nu))) return r;
+    HIPCHK(hipMemcpyAsync(c->d_epos, c->h_epos.data(), sizeof(int2) * ne, hipMemcpyHostToDevice, c->stream), "copy ep");
+    HIPCHK(hipMemcpyAsync(c->d_cell_ep, c->h_cell_ep.data(), sizeof(int2) * nu, hipMemcpyHostToDevice, c->stream),
+           "copy cell ep");
+    Params E = P;
+    E.mode = 2; E.epos = c->d_epos; E.n_ep = ne; E.ept = c->d_ept; E.n_cells = (ne + 1) / 2; E.ctrace = nullptr;
+    if ((r = launch_blocks(c, E, E.n_cells))) return r;
+    P.ept = c->d_ept; P.cell_ep = c->d_cell_ep;
+    c->n_ep_saved += (unsigned long long)(2 * nu - ne);
+  }
+  if ((r = launch_blocks(c, P, nu))) return r;
+  HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
   if (P.ivhist) {  // re-plan the LDS window from the measured histogram
     const int nkey = c->n_coarse + 2;
     std::vector<unsigned long long> hk((size_t)nkey * c->n_iv), h(c->n_iv, 0);
@@ -1594,61 +1699,29 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
       for (int j = 0; j < c->n_iv; j++) h[j] += hk[(size_t)k * c->n_iv + j];
     choose_window(c, std::vector<double>(h.begin(), h.end()));
     c->hist_pending = false;
-    if (getenv("FSCLG_DEBUG_PLAN")) {  // development aid: coverage of the best window by size
-      double tot = 0;
-      for (auto v : h) tot += (double)v;
-      fprintf(stderr, "fsclg plan: window [%d, %d) covers %.3f\n", c->c_ivc0, c->c_ivc0 + c->c_civ, c->c_cover);
-      for (int K : {8, 16, 21, 32, 48, 64, 96, 128}) {
-        double best = 0, run = 0;
-        for (int j = 0; j < c->n_iv; j++) {
-          run += (double)h[j];
-          if (j >= K) run -= (double)h[j - K];
-          best = std::max(best, run);
-        }
-        fprintf(stderr, "  K=%3d covers %.3f\n", K, best / tot);
-      }
-      for (int k = 0; k < nkey; k++) {  // per phase key: weight, best-window coverage at the planned K
-        double kt = 0, best = 0, run = 0;
-        for (int j = 0; j < c->n_iv; j++) kt += (double)hk[(size_t)k * c->n_iv + j];
-        if (kt <= 0) continue;
-        for (int j = 0; j < c->n_iv; j++) {
-          run += (double)hk[(size_t)k * c->n_iv + j];
-          if (j >= c->c_civ) run -= (double)hk[(size_t)k * c->n_iv + j - c->c_civ];
-          best = std::max(best, run);
-        }
-        fprintf(stderr, "  key %2d: weight %.3f, own best window covers %.3f\n", k, kt / tot, best / kt);
-      }
-      for (int j = 0; j < c->n_iv; j += 10) {
-        double sub = 0;
-        for (int k = j; k < std::min(j + 10, c->n_iv); k++) sub += (double)h[k];
-        fprintf(stderr, "  iv %3d..%3d: %.3f\n", j, j + 9, sub / tot);
-      }
-    }
   }
   if (P.ctrace) {  // development aid: append [n, then n x (start, end, cu, terms, 4 phase times)] to the file
-    std::vector<unsigned long long> h((size_t)8 * n_cells);
+    std::vector<unsigned long long> h((size_t)8 * nu);
     HIPCHK(hipMemcpyAsync(h.data(), P.ctrace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream),
            "copy trace");
     HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     if (FILE* f = fopen(getenv("FSCLG_CELL_TRACE"), "ab")) {
-      const unsigned long long nn = (unsigned long long)n_cells;
+      const unsigned long long nn = (unsigned long long)nu;
       fwrite(&nn, sizeof nn, 1, f);
       fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
       fclose(f);
     }
   }
-  c->h_out.resize(n_cells);
-  HIPCHK(hipMemcpyAsync(c->h_out.data(), c->d_out, sizeof(fsclg_point_t) * n_cells, hipMemcpyDeviceToHost, c->stream),
+  c->h_out.resize(nu);
+  HIPCHK(hipMemcpyAsync(c->h_out.data(), c->d_out, sizeof(fsclg_point_t) * nu, hipMemcpyDeviceToHost, c->stream),
          "copy out");
   HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
   c->kernel_ms += ms;
   c->launches++;
-  for (int k = 0; k < n_cells; k++) {
-    out[c->h_order[k]] = c->h_out[k];
-    c->cell_cost[key(c->h_cells[k])] = c->h_out[k].cost;
-  }
+  for (int k = 0; k < nu; k++) c->cell_cost[key(c->h_cells[k])] = c->h_out[k].cost;
+  for (int i = 0; i < n_cells; i++) out[i] = c->h_out[c->h_upos[c->h_uidx[i]]];
   for (int i = 0; i < n_cells; i++)
     if (out[i].flags) return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL, "device flag");
   return FSCLG_OK;
