@@ -187,7 +187,8 @@ def main() -> int:
         "stats": {k: st[k] for k in ("n_terms", "n_null", "n_walks", "n_unsafe", "n_slow", "n_ties", "trials",
                                      "host_perm_s", "scan_s", "permute_s", "gp_evals",
                                      "cache_iv0", "cache_n_iv", "cache_n_rows", "cache_cover", "window_ms",
-                                     "host_null_s", "host_upload_s", "search_s", "prune_s")},
+                                     "host_null_s", "host_upload_s", "search_s", "prune_s", "n_dup_cells",
+                                     "n_ep_saved")},
     }
 
     # ---- CPU baseline: the oracle port on the host cores, bounded sample = the initial scan

@@ -77,7 +77,8 @@ class Stats(C.Structure):  # fscl_amd_stats_t
                 ("n_launches", C.c_ulonglong), ("negj", C.c_ulonglong), ("trials", C.c_int),
                 ("cache_iv0", C.c_int), ("cache_n_iv", C.c_int), ("cache_n_rows", C.c_int),
                 ("cache_cover", C.c_double), ("window_ms", C.c_double), ("host_null_s", C.c_double),
-                ("host_upload_s", C.c_double), ("search_s", C.c_double), ("prune_s", C.c_double)]
+                ("host_upload_s", C.c_double), ("search_s", C.c_double), ("prune_s", C.c_double),
+                ("n_dup_cells", C.c_ulonglong), ("n_ep_saved", C.c_ulonglong)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1769,6 +1769,7 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
   st->n_terms = h[0]; st->n_null = h[1]; st->n_walks = h[2]; st->n_maxalpha = h[3];
   st->n_unsafe = h[4]; st->n_slow = h[5]; st->n_ties = h[6]; st->n_cells = h[7];
   st->kernel_ms = c->kernel_ms; st->n_launches = c->launches; st->window_ms = c->window_ms;
+  st->n_dup_cells = c->n_dup_cells; st->n_ep_saved = c->n_ep_saved;
   if (c->plan_dirty) plan_cache(c);
   st->cache_iv0 = c->c_ivc0; st->cache_n_iv = c->c_civ; st->cache_n_rows = c->c_crow; st->cache_cover = c->c_cover;
   return FSCLG_OK;
@@ -1778,7 +1779,7 @@ int fsclg_reset_stats(fsclg_ctx* c) {
   if (!c) return set_err(FSCLG_E_ARG, "stats");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
-  c->kernel_ms = 0.0; c->launches = 0; c->window_ms = 0.0;
+  c->kernel_ms = 0.0; c->launches = 0; c->window_ms = 0.0; c->n_dup_cells = 0; c->n_ep_saved = 0;
   return FSCLG_OK;
 }
 

@@ -695,6 +695,7 @@ void fscl_amd_get_stats(fscl_amd_stats_t *st) {
       st->n_unsafe = g.n_unsafe; st->n_slow = g.n_slow; st->n_ties = g.n_ties; st->n_launches = g.n_launches;
       st->cache_iv0 = g.cache_iv0; st->cache_n_iv = g.cache_n_iv; st->cache_n_rows = g.cache_n_rows;
       st->cache_cover = g.cache_cover; st->window_ms = g.window_ms;
+      st->n_dup_cells = g.n_dup_cells; st->n_ep_saved = g.n_ep_saved;
     }
   }
 }

@@ -173,6 +173,7 @@ typedef struct {
   double host_upload_s;   /*   rows + null sums to the device */
   double search_s;        /*   cell evaluation (launch, kernel, results, rank exchange) */
   double prune_s;         /*   pruning and bookkeeping */
+  unsigned long long n_dup_cells, n_ep_saved;  /* fsclg_stats_t: work shared between cells */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

@@ -66,6 +66,8 @@ typedef struct {
   int cache_iv0, cache_n_iv, cache_n_rows;  /* LDS coefficient window: intervals, device rows */
   double cache_cover;              /* its planned share of the terms */
   double window_ms;                /* summed duration of the window null-sum kernels (HIP events) */
+  unsigned long long n_dup_cells;  /* cells answered by an identical cell of the same launch */
+  unsigned long long n_ep_saved;   /* endpoint evaluations saved by sharing between neighbouring cells */
 } fsclg_stats_t;
 
 int fsclg_open(int device, fsclg_ctx **out);

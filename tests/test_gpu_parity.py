@@ -113,6 +113,24 @@ def test_windowed_null_sums_match_oracle(built, tmp, name, er, parts, opts):
     assert fscl_amd.get_stats()["window_ms"] > 0
 
 
+def test_shared_cells_and_endpoints_match_oracle(built, tmp):
+    """First SNP half a grid step in: neighbouring scan points often share one G-aligned
+    permutation cell (scan-chromosome.c:481-486), and every scan cell shares its endpoints
+    with its neighbours; both are evaluated once on the device (fsclg_search_maxpos)."""
+    chrs = []
+    for name, off, seed in (("a", 1_250_000, 61), ("b", 3_030_000, 62)):
+        (nm, pos, k, nn, fold), = synth.generate(n_chr=1, chr_len=6_000_000, snps_per_chr=5000, n=30, seed=seed,
+                                                  sweeps_per_chr=1, chr_names=[name])
+        chrs.append((nm, pos + off, k, nn, fold))
+    snp = tmp / "shared.snp"
+    synth.write_snp_file(str(snp), chrs)
+    opts = ["--coarse-grid-spacing=50000", "--n-permute=6"]
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), "shared")
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+
+
 def test_ms_input_matches_oracle_on_converted_file(built, tmp):
     ms = tmp / "x.ms"
     synth.write_ms_file(str(ms), n_blocks=4, n_hap=20, n_seg=600, seed=41)
