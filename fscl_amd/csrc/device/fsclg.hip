@@ -29,6 +29,7 @@
 
 #include <vector>
 #include <algorithm>
+#include <type_traits>
 #include <unordered_map>
 
 #include "../../../include/fsclg.h"
@@ -62,7 +63,7 @@ constexpr int NWAVE = WG / 64;
 #endif
 constexpr int SEG = FSCLG_SEG;     // terms per work segment
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
-constexpr int MAXSEG_W = 192;      // segments per walk (161 at 163841 terms)
+constexpr int MAXSEG_W = (163841 / SEG + 2 + 31) / 32 * 32;  // segments per walk (82 at 163841 terms)
 constexpr int SEGWORDS = MAXSEG_W / 32;
 constexpr int MAXTIES = 512;       // per eval_walks; overflow sends the affected argmax to the exact slow path
 constexpr int MAXREF = 16;
@@ -86,7 +87,7 @@ struct Params {
   const uint2* prs;            // [blocks * BLK + PAD] the same sites, each aligned BLK-block sorted by row:
                                // (position ^ POS_BIAS, row | offset in block << 16); null: no sorted path
   const double* logt3;         // [3][65536]: c_b + log_table[i], the three branches of sm-search.c:40-46
-  const double* coef;          // [n_iv][n_rows + 1][4], device row 0 all zero (sentinel)
+  const double* coef;          // [n_iv][2 planes][n_rows + 1][2] (coef_off), device row 0 all zero (sentinel)
   const double* nullrow;       // [n_rows + 1], entry 0 zero
   const double* thr;           // thr[j] = least x with (int)((x - LOG_AD_MIN) / step) >= j, j = 1..n_iv-1
   const int32_t* chr_start;
@@ -105,6 +106,7 @@ struct Params {
   int n_iv;
   int n_rows;
   int stride;                  // n_rows + 1
+  int pstride;                 // bytes from plane A to plane B of an interval: stride * 16
   double step;
   double inv_step;
   double iv_off;               // -LOG_AD_MIN * inv_step - 1e-9 (interval_of)
@@ -234,20 +236,28 @@ __device__ __forceinline__ double null_of(uint32_t r, const Smem& S, const Param
   else return P.nullrow[r];
 }
 
-// coefficient block of (row, interval): interval-major [iv][row][4], so the lanes of a
-// wave (neighbouring sites, nearly equal log distance) read from one interval's rows;
-// 32-bit byte offset (the table is < 4 GiB, checked on upload)
-__device__ __forceinline__ const double2* coef_of(uint32_t r, int iv, const Params& P) {
+// coefficient block of (row, interval).  Layout [iv][plane][row][2]: per interval, plane A
+// holds (c0, c1) of every row and plane B (c2, c3), 16 B per entry, so in a ds_read_b128 the
+// rows of a 16-lane group fall on 16 distinct 4-bank slots (a 32-B block per row gave 8),
+// halving the expected bank conflicts of the random-row gathers; interval-major, so the lanes
+// of a wave (neighbouring sites, nearly equal log distance) read from one interval.  The
+// byte offset of (iv, r) in plane A is (iv * stride) * 32 + r * 16, plane B adds
+// P.pstride = stride * 16; 32-bit offsets (the table is < 4 GiB, checked on upload).
+__device__ __forceinline__ uint32_t coef_off(uint32_t r, int iv, const Params& P) {
 #ifdef FSCLG_EXP_COEFCONST  // timing ablation only (wrong results): one block per interval parity
-  return reinterpret_cast<const double2*>(P.coef) + (iv & 1) * 2;
+  return (uint32_t)(iv & 1) << 4;
 #endif
-  const uint32_t off = (__umul24((uint32_t)iv, (uint32_t)P.stride) + r) << 5;
-  return reinterpret_cast<const double2*>(reinterpret_cast<const char*>(P.coef) + off);
+  return (__umul24((uint32_t)iv, (uint32_t)P.stride) << 5) + (r << 4);
+}
+
+__device__ __forceinline__ void coef_ld(const char* base, uint32_t off, const Params& P, double2& a, double2& b) {
+  a = *reinterpret_cast<const double2*>(base + off);
+  b = *reinterpret_cast<const double2*>(base + off + (uint32_t)P.pstride);
 }
 
 // the coefficient block of (row, interval) into a = (c0, c1), b = (c2, c3): from the LDS
-// planes when (interval, row) lies in the cached window (planned on the host from sampled
-// walks and row frequencies, fsclg_plan_cache), from the global table otherwise
+// window when (interval, row) lies in it (every row of intervals [ivc0, ivc0 + n_civ)),
+// from the global table otherwise
 template <bool LDS>
 __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, const Params& P, double2& a, double2& b) {
 #ifdef FSCLG_NOCACHE  // experiment: coefficients always from the global table
@@ -257,18 +267,10 @@ __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, co
 #endif
     const uint32_t ci = (uint32_t)(iv - S.ivc0);
     const bool hit = ci < (uint32_t)P.n_civ;  // every row is cached
-    const uint32_t li = __umul24(min(ci, (uint32_t)P.civ_max), (uint32_t)P.stride) + r;
-    a = reinterpret_cast<const double2*>(fsclg_dyn)[2 * li];
-    b = reinterpret_cast<const double2*>(fsclg_dyn)[2 * li + 1];
-    if (!hit) {
-      const double2* cp = coef_of(r, iv, P);
-      a = cp[0];
-      b = cp[1];
-    }
+    coef_ld(fsclg_dyn, coef_off(r, (int)min(ci, (uint32_t)P.civ_max), P), P, a, b);
+    if (!hit) coef_ld(reinterpret_cast<const char*>(P.coef), coef_off(r, iv, P), P, a, b);
   } else {
-    const double2* cp = coef_of(r, iv, P);
-    a = cp[0];
-    b = cp[1];
+    coef_ld(reinterpret_cast<const char*>(P.coef), coef_off(r, iv, P), P, a, b);
   }
 }
 
@@ -276,36 +278,28 @@ __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, co
 // then per term the LDS window or, for lanes outside it, the global table
 template <bool LDS>
 __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t (&rv)[U], const Smem& S,
-                                           const Params& P, int ivc0, double2 (&ca)[U], double2 (&cb)[U]) {
+                                           const Params& P, int ivc0, double2 (&ca)[U], double2 (&cb)[U],
+                                           int (&iv)[U]) {
 #ifdef FSCLG_NOCACHE
   constexpr bool CACHE = false;
 #else
   constexpr bool CACHE = LDS;
 #endif
-  int iv[U];
 #pragma unroll
   for (int u = 0; u < U; u++) iv[u] = interval_of<LDS>(x[u], S, P);
   if constexpr (CACHE) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t ci = (uint32_t)(iv[u] - ivc0);
-      if (ci < (uint32_t)P.n_civ) {  // every row is cached
-        const double2* lp = reinterpret_cast<const double2*>(fsclg_dyn) + 2 * (__umul24(ci, (uint32_t)P.stride) + rv[u]);
-        ca[u] = lp[0];
-        cb[u] = lp[1];
-      } else {
-        const double2* cp = coef_of(rv[u], iv[u], P);
-        ca[u] = cp[0];
-        cb[u] = cp[1];
-      }
+      if (ci < (uint32_t)P.n_civ)  // every row is cached
+        coef_ld(fsclg_dyn, coef_off(rv[u], (int)ci, P), P, ca[u], cb[u]);
+      else
+        coef_ld(reinterpret_cast<const char*>(P.coef), coef_off(rv[u], iv[u], P), P, ca[u], cb[u]);
     }
   } else {
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const double2* cp = coef_of(rv[u], iv[u], P);
-      ca[u] = cp[0];
-      cb[u] = cp[1];
-    }
+    for (int u = 0; u < U; u++)
+      coef_ld(reinterpret_cast<const char*>(P.coef), coef_off(rv[u], iv[u], P), P, ca[u], cb[u]);
   }
 }
 
@@ -331,14 +325,40 @@ __device__ __forceinline__ long long wave_sum64(long long v) {
   return v;
 }
 
-// init_scan_result (scan-chromosome.c:58-101) for one point, one thread
-__device__ __forceinline__ void init_point(Pt& pt, int chr, int pos, const Params& P) {
-  const int a = P.chr_start[chr], n = P.chr_n[chr];
-  int i = 0, j = n;
-  while (j - i > 1) {  // search_snppos, scan-chromosome.c:39-56
-    const int m = (i + j) / 2;
-    if (pos_at(P, a + m) < pos) i = m; else j = m;
+// Narrow the open range (lo, hi) of a predicate T that holds on a prefix of it (lo counts as
+// true, hi as false) to hi = lo + 1 with an aligned group of G lanes of one wave: each round
+// probes G indices spread over (lo, hi), so ceil(log_{G+1}(hi - lo)) dependent rounds instead
+// of log2.  Every lane of the wave calls it (groups with nothing to search pass hi = lo + 1).
+// Returns hi, the first index where T is false.
+template <int G, typename F>
+__device__ __forceinline__ int group_search(int lo, int hi, int lane, F pred) {
+  const int j = lane & (G - 1), sh = lane & (64 - G);
+  for (;;) {
+    const bool act = hi - lo > 1;
+    if (!__any(act)) break;
+    const long long span = (long long)(hi - lo - 1);
+    bool t = false;
+    if (act) t = pred(lo + 1 + (int)((span * j) / G));
+    const unsigned long long b = __ballot(t);
+    if (act) {
+      const unsigned long long gm = G == 64 ? b : ((b >> sh) & ((1ull << G) - 1));
+      const int c = __popcll(gm);  // the probes are nondecreasing: T holds on the first c
+      const int nlo = c > 0 ? lo + 1 + (int)((span * (c - 1)) / G) : lo;
+      const int nhi = c < G ? lo + 1 + (int)((span * c) / G) : hi;
+      lo = nlo; hi = nhi;
+    }
   }
+  return hi;
+}
+
+// init_scan_result (scan-chromosome.c:58-101) for one point by one wave: search_snppos
+// (scan-chromosome.c:39-56) ends with j = the least index in [1, n) whose position is >= pos
+// (n if none) and i = j - 1; a 64-way search finds the same j
+__device__ __forceinline__ void init_point_wave(Pt& pt, int chr, int pos, const Params& P, int lane) {
+  const int a = P.chr_start[chr], n = P.chr_n[chr];
+  const int j = group_search<64>(0, n, lane, [&](int m) { return pos_at(P, a + m) < pos; });
+  if (lane != 0) return;
+  const int i = j - 1;
   int near;
   if (j == n) near = n - 1;
   else if ((long long)pos - pos_at(P, a + i) < (long long)pos_at(P, a + j) - pos) near = i;
@@ -358,8 +378,6 @@ __device__ __forceinline__ void init_point(Pt& pt, int chr, int pos, const Param
   pt.chr = chr; pt.nearest = near; pt.sweep = pos; pt.wstart = ws; pt.wend = we;
   pt.n_snps = we - ws + 1;
   pt.flags = 0;
-  // scan-chromosome.c:92-94 (sequential sum from 0.0 over the window): the whole
-  // chromosome's per trial from the host, a proper window's from window_null_kernel
   pt.N = (ws == cs && we == ce) ? P.chr_null[chr] : P.win_null[ws];
 }
 
@@ -376,36 +394,39 @@ __device__ __forceinline__ void set_binade(Pt& pt) {
   pt.inv_u = __longlong_as_double((long long)(1023 + 52 - e) << 52);
 }
 
-// the walk's index range: monotone predicate log(alpha d) > 4 on each side
-__device__ __forceinline__ void walk_bounds(Walk& W, const Pt& pt, const Params& P, int side) {
+// walk_bounds for every walk side of the phase: 8 lanes per (walk, side), a 9-way search
+// of the same monotone predicates (left: log(alpha d) > 4 holds on a prefix of
+// (wstart - 1, near); right, when the first right neighbour is inside: its negation holds on
+// a prefix of (near + 1, wend + 1))
+__device__ __forceinline__ void walk_bounds_par(Smem& S, const Params& P, int tid, int nw) {
+  const int lane = tid & 63, g = tid >> 3;
+  const bool act = g < 2 * nw;
+  const int w = act ? g >> 1 : 0, side = g & 1;
+  const Walk& W = S.w[w];
+  const Pt& pt = S.pt[act ? W.p : 0];
   const int near = pt.nearest, sweep = pt.sweep;
   const double la = W.la;
-  if (side == 0) {
-    if (log_ad_of(near, sweep, la, P) > LOG_AD_MAX) { W.len = 0; }
-    else W.len = 1;
-    // left: the ok-set is a suffix [L, near-1]
-    int a = pt.wstart - 1, b = near;
-    if (near - 1 >= pt.wstart) {
-      while (b - a > 1) {
-        const int m = a + (b - a) / 2;
-        if (log_ad_of(m, sweep, la, P) > LOG_AD_MAX) a = m; else b = m;
-      }
+  int lo = 0, hi = 1;
+  bool ok1 = false;
+  if (act) {
+    if (side == 0) { lo = pt.wstart - 1; hi = near; }
+    else {
+      ok1 = near + 1 <= pt.wend && !(log_ad_of(near + 1, sweep, la, P) > LOG_AD_MAX);
+      if (ok1) { lo = near + 1; hi = pt.wend + 1; }
     }
-    W.nl = near - b;
-    W.xl = log_ad_of(b < near ? b : near, sweep, la, P);
-  } else {
-    // right: first element may violate alone (de-collision shift), otherwise the ok-set is a prefix
-    int r = near;
-    if (near + 1 <= pt.wend && !(log_ad_of(near + 1, sweep, la, P) > LOG_AD_MAX)) {
-      int a = near + 1, b = pt.wend + 1;
-      while (b - a > 1) {
-        const int m = a + (b - a) / 2;
-        if (log_ad_of(m, sweep, la, P) > LOG_AD_MAX) b = m; else a = m;
-      }
-      r = a;
+  }
+  const int e = group_search<8>(lo, hi, lane, [&](int m) { return (log_ad_of(m, sweep, la, P) > LOG_AD_MAX) != (side == 1); });
+  if (act && (tid & 7) == 0) {
+    Walk& V = S.w[w];
+    if (side == 0) {
+      V.len = log_ad_of(near, sweep, la, P) > LOG_AD_MAX ? 0 : 1;
+      V.nl = near - e;
+      V.xl = log_ad_of(e < near ? e : near, sweep, la, P);
+    } else {
+      const int r = ok1 ? e - 1 : near;
+      V.nr = r - near;
+      V.xr = log_ad_of(r, sweep, la, P);
     }
-    W.nr = r - near;
-    W.xr = log_ad_of(r, sweep, la, P);
   }
 }
 
@@ -450,6 +471,14 @@ __device__ __forceinline__ int seg_of(const Walk& W, const Pt& pt, int i) {
 }
 
 __device__ __forceinline__ bool odd_int(double v) { return v - 2.0 * floor(0.5 * v) != 0.0; }
+
+// a wave-uniform double into scalar registers
+__device__ __forceinline__ double uniform_f64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 
 // one segment of one walk, by one wave: U terms per lane per trip with all loads issued
 // first.  Index order (SORTED = false): the segment's sites in order; lanes past it read
@@ -525,7 +554,8 @@ __device__ __forceinline__ void run_segment(Smem& S, int w, int s, const Params&
       atomicAdd(&P.ivhist[S.hkey * P.n_iv + interval_of<LDS>(x[0], S, P)], (unsigned long long)(ie - ib));
 #endif
     double2 ca[U], cb[U];
-    coef_stage<LDS>(x, rv, S, P, ivc0, ca, cb);
+    int ivs[U];
+    coef_stage<LDS>(x, rv, S, P, ivc0, ca, cb, ivs);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
@@ -552,6 +582,108 @@ __device__ __forceinline__ void run_segment(Smem& S, int w, int s, const Params&
   }
   // the segment's parity: sum over lanes of (sum mod 2); partials are exact integers
   // whenever the walk passes its flush check (otherwise its value is discarded)
+  const unsigned long long odd = __ballot(odd_int(sum));
+  if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
+  acc += sum;
+  accm += mag;
+}
+
+// run_segment for index-order segments with a wave-uniform spline interval.  Along a segment
+// the sites move monotonically away from (or towards) the sweep, and a trip's 64*U sites
+// usually span a small fraction of one interval, so the wave carries the interval civ of its
+// last site with its exact bounds [thr[civ], thr[civ+1]) in scalar registers: when every
+// lane's x lies inside (two compares per term) the interval is civ for all of them, with no
+// per-lane interval arithmetic, and the coefficient block comes from one place (the LDS
+// window or the global table, a uniform branch).  Otherwise the trip takes the per-lane path
+// of run_segment and re-centres civ on its last site.  Only the final trip of a segment
+// masks lanes past its end (zero sentinel row).
+template <bool LDS>
+__device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Params& P, int lane, double& acc,
+                                                double& accm) {
+#ifdef FSCLG_EXP_NOTERMS
+  return;
+#endif
+  const Walk& W = S.w[w];
+  const Pt& pt = S.pt[W.p];
+  const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS;
+  const double la = W.la, inv = pt.inv_u;
+  const int lo = pt.nearest - W.nl;
+  int ib, ie;
+  seg_bounds(W, pt, s, ib, ie);
+  const int n = ie - ib;
+  const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
+  const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
+  int civ = 0;
+  double tlo = __builtin_inf(), thi = -__builtin_inf();  // empty: the first trip takes the per-lane path
+  double sum = 0.0, mag = 0.0;
+  auto trip = [&](const int kb, auto maskc) {
+    constexpr bool MASK = decltype(maskc)::value;
+    uint32_t pv[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int k = kb + 64 * u + lane;
+      const uint2 v = ld_pr(P.pr, (uint32_t)(ib + k));
+      pv[u] = v.x;
+      rv[u] = (!MASK || k < n) ? v.y : 0u;  // zero sentinel row past the segment
+    }
+    double x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = logt_lds<LDS>(absdist(pv[u], usweep), P) + la;
+    bool in = true;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const bool ok = (x[u] >= tlo) && (x[u] < thi);
+      in = in && (MASK ? (ok || kb + 64 * u + lane >= n) : ok);  // masked lanes add exactly 0 anyway
+    }
+    double2 ca[U], cb[U];
+#ifdef FSCLG_PATHSTATS  // diagnostic: trips per path in the stats slots 4 (per-lane), 5 (LDS), 6 (global)
+    if (lane == 0) {
+      const bool al = __all(in);
+      atomicAdd(&S.cnt[!al ? 4 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 5 : 6)], 1ull);
+    }
+#endif
+    if (__all(in)) {
+      const uint32_t ci = (uint32_t)(civ - ivc0);
+      if (LDS && ci < (uint32_t)P.n_civ) {
+        const char* lb = fsclg_dyn + (__umul24(ci, (uint32_t)P.stride) << 5);
+#pragma unroll
+        for (int u = 0; u < U; u++) coef_ld(lb, rv[u] << 4, P, ca[u], cb[u]);
+      } else {
+        const char* gb = reinterpret_cast<const char*>(P.coef) + (__umul24((uint32_t)civ, (uint32_t)P.stride) << 5);
+#pragma unroll
+        for (int u = 0; u < U; u++) coef_ld(gb, rv[u] << 4, P, ca[u], cb[u]);
+      }
+    } else {
+      int iv[U];
+      coef_stage<LDS>(x, rv, S, P, ivc0, ca, cb, iv);
+      civ = __builtin_amdgcn_readlane(iv[U - 1], 63);  // the trip's last site
+      tlo = uniform_f64(thrp[civ]);
+      thi = uniform_f64(thrp[civ + 1]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
+      const double q = (y - null_of<LDS>(rv[u], S, P)) * inv;
+      const double R = rint(q);                 // the even neighbour at a tie; the resolver settles ties
+      const double fr = q - R;
+      if (__ballot(fabs(fr) == 0.5)) {          // rare: record the tie with its in-segment prefix parity
+        const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        const unsigned long long ps = __ballot(odd_int(sum));
+        const unsigned long long pr = __ballot(odd_int(R));
+        const int pre = (__popcll(ps) + __popcll(pr & below)) & 1;
+        if (fabs(fr) == 0.5) {
+          const int ti = atomicAdd(&S.n_ties, 1);
+          if (ti < MAXTIES)
+            S.ties[ti] = (w << 20) | ((fr < 0.0 ? 1 : 0) << 19) | (pre << 18) | (ib + kb + 64 * u + lane - lo);
+        }
+      }
+      sum += R;
+      mag += fabs(R);
+    }
+  };
+  int kb = 0;
+  for (; kb + 64 * U <= n; kb += 64 * U) trip(kb, std::false_type{});
+  if (kb < n) trip(kb, std::true_type{});
   const unsigned long long odd = __ballot(odd_int(sum));
   if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
   acc += sum;
@@ -672,13 +804,7 @@ __device__ __forceinline__ void load_window(Smem& S, const Params& P, int wb) {
 template <bool LDS>
 __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nw = S.nwalk;
-  if (tid < 2 * nw) walk_bounds(S.w[tid >> 1], S.pt[S.w[tid >> 1].p], P, tid & 1);
-  if (tid < nw) {
-    S.P[tid] = 0; S.Q[tid] = 0; S.wflag[tid] = 0; S.need_slow[tid] = 0;
-    for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = 0;
-  }
-  if (tid == 0) S.n_ties = 0;
+  const int nw = __builtin_amdgcn_readfirstlane(S.nwalk);
 #ifdef FSCLG_PHASE_TIMING
   unsigned long long t0 = 0;
   if (tid == 0) t0 = wall_clock64();
@@ -686,9 +812,16 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
 #else
 #define PHASE_MARK(k) do { } while (0)
 #endif
+  walk_bounds_par(S, P, tid, nw);
+  if (tid < nw) {
+    S.P[tid] = 0; S.Q[tid] = 0; S.wflag[tid] = 0; S.need_slow[tid] = 0;
+    for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = 0;
+  }
+  if (tid == 0) S.n_ties = 0;
   __syncthreads();
   PHASE_MARK(0);
   TRACE("  bounds done: nw=%d w0 len=%d nl=%d nr=%d\n", nw, S.w[0].len, S.w[0].nl, S.w[0].nr);
+#ifdef FSCLG_SERIAL_LAYOUT  // A/B: the layout by thread 0
   if (tid == 0) {
     int seg = 0;
     unsigned long long terms = 0;
@@ -735,6 +868,66 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
     S.cnt[0] += terms;
     S.cnt[2] += nw;
   }
+#else
+  // layout by wave 0, one lane per walk (nw <= MAXWALK = 32), values in registers
+  if (wave == 0) {
+    const bool act = lane < nw;
+    const int K = P.n_civ;
+    int len = 0, wb = -1, nseg = 0;  // empty walks (wb = -1) sort last and open no group
+    if (act) {
+      Walk& W = S.w[lane];
+      len = W.len ? 1 + W.nl + W.nr : 0;
+      // the walk's window: the n_civ intervals below the one of its largest x (the site
+      // count of a long walk grows like e^x up to there)
+      if (LDS && K > 0 && len) {
+        const int top = interval_of<LDS>(fmax(W.xl, W.xr), S, P);
+        wb = min(max(top - K + 1, 0), P.n_iv - K);
+      }
+      const int srt = (P.prs != nullptr && len >= SORT_MIN) ? 1 : 0;
+      const int near = S.pt[W.p].nearest, lo = near - W.nl, hi = near + W.nr;
+      int nsl;
+      if (!len) { nsl = 0; nseg = 0; }
+      else if (!srt) { nsl = (W.nl + SEG) / SEG; nseg = nsl + (W.nr + SEG - 1) / SEG; }
+      else {
+        nsl = (near >> BLK_LOG) - (lo >> BLK_LOG) + 1;
+        nseg = nsl + (W.nr ? (hi >> BLK_LOG) - ((near + 1) >> BLK_LOG) + 1 : 0);
+      }
+      W.len = len; W.wb = wb; W.srt = srt; W.nsl = nsl; W.nseg = nseg;
+    }
+    // walks in descending window base, stable: each walk's rank and first segment
+    int rank = 0, seg0 = 0;
+    for (int j = 0; j < nw; j++) {
+      const int wbj = __shfl(wb, j, 64), nsj = __shfl(nseg, j, 64);
+      const bool before = wbj > wb || (wbj == wb && j < lane);
+      rank += before ? 1 : 0;
+      seg0 += before ? nsj : 0;
+    }
+    if (act) { S.w[lane].seg0 = seg0; S.word[rank] = lane; }
+    // a group shares the window of its first walk and takes the following walks whose base
+    // is at most 2 below it (they lose at most their two sparsest intervals)
+    int ng = 0, gprev = 0;
+    for (int k = 0; k < nw; k++) {
+      const int l = __ffsll((unsigned long long)__ballot(act && rank == k)) - 1;
+      const int wbk = __shfl(wb, l, 64), lenk = __shfl(len, l, 64), s0k = __shfl(seg0, l, 64);
+      if (lenk && (ng == 0 || wbk < gprev - 2)) {
+        if (lane == 0) { S.gwb[ng] = wbk; S.gseg[ng] = s0k; }
+        ng++;
+        gprev = wbk;
+      }
+    }
+    int tot = nseg;
+    long long terms = len;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { tot += __shfl_xor(tot, o, 64); terms += __shfl_xor(terms, o, 64); }
+    if (lane == 0) {
+      S.gseg[ng] = tot;
+      S.ngrp = ng;
+      S.seg_total = tot;
+      S.cnt[0] += (unsigned long long)terms;
+      S.cnt[2] += nw;
+    }
+  }
+#endif
   __syncthreads();
   PHASE_MARK(1);
   TRACE("  layout done: segs=%d\n", S.seg_total);
@@ -764,7 +957,11 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
       if (S.w[w].srt) run_segment<LDS, true>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
       else
 #endif
+#ifdef FSCLG_LANE_IV  // A/B: per-lane interval on every trip
       run_segment<LDS, false>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+#else
+      run_segment_idx<LDS>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+#endif
      }
     }
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
@@ -905,7 +1102,7 @@ template <bool LDS>
 #endif
 __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P) {
   __shared__ Smem S;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous run of cells
   // cells arrive in the host's longest-first order; the hardware dispatches blocks in order
   // (round-robin over the XCDs), so the long cells start first and spread over the XCDs
@@ -938,7 +1135,7 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
   } else if (P.mode == 2) {
     // distinct cell endpoints, two per block: scan-chromosome.c:130-134 for each
     const int e0 = 2 * cell, np = min(2, P.n_ep - e0);
-    if (tid < np) init_point(S.pt[tid], P.epos[e0 + tid].x, P.epos[e0 + tid].y, P);
+    if (wave < np) init_point_wave(S.pt[wave], P.epos[e0 + wave].x, P.epos[e0 + wave].y, P, lane);
     __syncthreads();
     if (tid == 0) for (int k = 0; k < np; k++) S.cnt[1] += (unsigned long long)S.pt[k].n_snps;
     search_maxalpha_pts<LDS>(S, P, 0, np);
@@ -949,7 +1146,7 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
       if (tid < 2) read_point(S.pt[tid], P.ept[tid == 0 ? P.cell_ep[cell].x : P.cell_ep[cell].y]);
       __syncthreads();
     } else {
-      if (tid < 2) init_point(S.pt[tid], c.chr, tid == 0 ? c.start_pos : c.end_pos, P);
+      if (wave < 2) init_point_wave(S.pt[wave], c.chr, wave == 0 ? c.start_pos : c.end_pos, P, lane);
       __syncthreads();
       if (tid == 0) S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps);
       search_maxalpha_pts<LDS>(S, P, 0, 2);  // start and end points share the two phases
@@ -959,9 +1156,9 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
       const int sp = S.pt[0].sweep, ep = S.pt[1].sweep;
       if (ep - sp <= P.bp_resl) break;
       if (++iter > 64) { if (tid == 0) S.pt[0].flags |= PF_NOCONV; break; }
-      if (tid == 0) {
-        init_point(S.pt[2], c.chr, (sp + ep) / 2, P);
-        S.cnt[1] += (unsigned long long)S.pt[2].n_snps;
+      if (wave == 0) {
+        init_point_wave(S.pt[2], c.chr, (sp + ep) / 2, P, lane);
+        if (lane == 0) S.cnt[1] += (unsigned long long)S.pt[2].n_snps;
       }
       __syncthreads();
       search_maxalpha_pts<LDS>(S, P, 2, 1);
@@ -1245,12 +1442,15 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
     }
   if ((r = upload(&c->d_logt, lt3.data(), lt3.size(), c->stream))) return r;
   c->h_lt3.swap(lt3);
-  // [row][iv][4] -> [iv][1 + row][4]: device row 0 is an all-zero sentinel (terms exactly 0)
+  // [row][iv][4] -> [iv][plane][1 + row][2] (coef_off): device row 0 is an all-zero sentinel
+  // (terms exactly 0); plane 0 holds (c0, c1), plane 1 (c2, c3)
   const size_t stride = (size_t)n_rows + 1;
   std::vector<double> tcoef(stride * n_iv * 4, 0.0);
   for (int rr = 0; rr < n_rows; rr++)
     for (int iv = 0; iv < n_iv; iv++)
-      memcpy(&tcoef[((size_t)iv * stride + rr + 1) * 4], coef + ((size_t)rr * n_iv + iv) * 4, sizeof(double) * 4);
+      for (int pl = 0; pl < 2; pl++)
+        memcpy(&tcoef[(((size_t)iv * 2 + pl) * stride + rr + 1) * 2], coef + ((size_t)rr * n_iv + iv) * 4 + 2 * pl,
+               sizeof(double) * 2);
   if ((r = upload(&c->d_coef, tcoef.data(), tcoef.size(), c->stream))) return r;
   std::vector<double> nul(1, 0.0);
   nul.insert(nul.end(), nullrow, nullrow + n_rows);
@@ -1524,7 +1724,7 @@ static void plan_cache(fsclg_ctx* c) {
 static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
   Params P;
   P.pr = c->d_pr; P.prs = c->d_prs; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
-  P.thr = c->d_thr; P.n_rows = c->n_rows; P.stride = c->n_rows + 1;
+  P.thr = c->d_thr; P.n_rows = c->n_rows; P.stride = c->n_rows + 1; P.pstride = P.stride * 16;
   P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step - 1e-9;
   // dynamic LDS: the planned coefficient window, thresholds and null rows
   if (c->plan_dirty) plan_cache(c);
@@ -1673,7 +1873,6 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
     HIPCHK(hipMemsetAsync(c->d_ivhist, 0, sizeof(unsigned long long) * nh, c->stream), "hipMemset ivhist");
     P.ivhist = c->d_ivhist;
   }
-  HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
   if (use_ep) {
     if ((r = ensure_buf(&c->d_epos, &c->epos_cap, ne))) return r;
     if ((r = ensure_buf(&c->d_ept, &c->ept_cap, ne))) return r;
@@ -1681,6 +1880,10 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
     HIPCHK(hipMemcpyAsync(c->d_epos, c->h_epos.data(), sizeof(int2) * ne, hipMemcpyHostToDevice, c->stream), "copy ep");
     HIPCHK(hipMemcpyAsync(c->d_cell_ep, c->h_cell_ep.data(), sizeof(int2) * nu, hipMemcpyHostToDevice, c->stream),
            "copy cell ep");
+  }
+  // the events bracket the kernel launches only (one or two of search_maxpos_kernel)
+  HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
+  if (use_ep) {
     Params E = P;
     E.mode = 2; E.epos = c->d_epos; E.n_ep = ne; E.ept = c->d_ept; E.n_cells = (ne + 1) / 2; E.ctrace = nullptr;
     if ((r = launch_blocks(c, E, E.n_cells))) return r;
@@ -1719,7 +1922,7 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
   c->kernel_ms += ms;
-  c->launches++;
+  c->launches += use_ep ? 2 : 1;
   for (int k = 0; k < nu; k++) c->cell_cost[key(c->h_cells[k])] = c->h_out[k].cost;
   for (int i = 0; i < n_cells; i++) out[i] = c->h_out[c->h_upos[c->h_uidx[i]]];
   for (int i = 0; i < n_cells; i++)
