@@ -611,24 +611,47 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
   int ib, ie;
   seg_bounds(W, pt, s, ib, ie);
   const int n = ie - ib;
+#ifdef FSCLG_EXP_NOPR
+  const uint32_t ex_p0 = P.pr[ib].x, ex_p1 = P.pr[max(ie - 1, ib)].x;
+#endif
   const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
   const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
   int civ = 0;
   double tlo = __builtin_inf(), thi = -__builtin_inf();  // empty: the first trip takes the per-lane path
   double sum = 0.0, mag = 0.0;
+#ifndef FSCLG_NO_PF
+  // the sites of the next trip are loaded one trip ahead (nx), issued after the trip's own
+  // coefficient loads so that waiting for a global coefficient gather (vmcnt counts in
+  // order) does not wait for them; PAD covers the look-ahead past a segment's end
+  uint2 nx[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) nx[u] = ld_pr(P.pr, (uint32_t)(ib + 64 * u + lane));
+#endif
   auto trip = [&](const int kb, auto maskc) {
     constexpr bool MASK = decltype(maskc)::value;
     uint32_t pv[U], rv[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int k = kb + 64 * u + lane;
+#ifdef FSCLG_EXP_NOPR  // timing ablation only (wrong results): sites interpolated, no (position, row) load
+      const uint2 v = make_uint2(ex_p0 + (uint32_t)(((long long)(ex_p1 - ex_p0) * k) / (n > 0 ? n : 1)),
+                                 1u + (((uint32_t)(ib + k) * 2654435761u) >> 27));
+#elif !defined(FSCLG_NO_PF)
+      const uint2 v = nx[u];
+#else
       const uint2 v = ld_pr(P.pr, (uint32_t)(ib + k));
+#endif
       pv[u] = v.x;
       rv[u] = (!MASK || k < n) ? v.y : 0u;  // zero sentinel row past the segment
     }
     double x[U];
 #pragma unroll
+#ifdef FSCLG_EXP_LTLDS  // timing ablation only (wrong results): every log distance from the LDS table
+    for (int u = 0; u < U; u++)
+      x[u] = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt)[256 + ((absdist(pv[u], usweep) >> 16) % (uint32_t)(P.lt_hi - 256))] + la;
+#else
     for (int u = 0; u < U; u++) x[u] = logt_lds<LDS>(absdist(pv[u], usweep), P) + la;
+#endif
     bool in = true;
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -637,13 +660,17 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
     }
     double2 ca[U], cb[U];
 #ifdef FSCLG_PATHSTATS  // diagnostic: trips per path in the stats slots 4 (per-lane), 5 (LDS), 6 (global)
+    const bool al = __all(in);
     if (lane == 0) {
-      const bool al = __all(in);
       atomicAdd(&S.cnt[!al ? 4 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 5 : 6)], 1ull);
     }
 #endif
     if (__all(in)) {
+#ifdef FSCLG_EXP_COEFLDS  // timing ablation only (wrong results): uniform trips always read the LDS window
+      const uint32_t ci = min((uint32_t)(civ - ivc0), (uint32_t)P.civ_max);
+#else
       const uint32_t ci = (uint32_t)(civ - ivc0);
+#endif
       if (LDS && ci < (uint32_t)P.n_civ) {
         const char* lb = fsclg_dyn + (__umul24(ci, (uint32_t)P.stride) << 5);
 #pragma unroll
@@ -660,10 +687,22 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
       tlo = uniform_f64(thrp[civ]);
       thi = uniform_f64(thrp[civ + 1]);
     }
+    double nul[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) nul[u] = null_of<LDS>(rv[u], S, P);
+#ifndef FSCLG_NO_PF
+    // after the last use of this trip's rows (so the look-ahead loads into the same
+    // registers, no copy at the loop edge), unconditional (the last trip's look-ahead reads
+    // the padding; a conditional load would make the waits below conservative at the join)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) nx[u] = ld_pr(P.pr, (uint32_t)(ib + kb + 64 * U + 64 * u + lane));
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
-      const double q = (y - null_of<LDS>(rv[u], S, P)) * inv;
+      const double q = (y - nul[u]) * inv;
       const double R = rint(q);                 // the even neighbour at a tie; the resolver settles ties
       const double fr = q - R;
       if (__ballot(fabs(fr) == 0.5)) {          // rare: record the tie with its in-segment prefix parity
