@@ -115,6 +115,7 @@ struct Params {
   int n_cache;                 // n_civ * stride blocks
   int off_thr, off_nul;        // byte offsets in fsclg_dyn (the coefficient window at 0)
   int off_lt, lt_hi;           // LDS copy of logt3 branch 2 (|d| > 2^24) entries [256, lt_hi) at off_lt; lt_hi 0: none
+  uint32_t lt_span;            // |d| is in that copy iff |d| - 2^24 < lt_span (unsigned); 0: none
   int eval_range;
   int bp_resl;
   int n_cells;
@@ -472,6 +473,13 @@ __device__ __forceinline__ int seg_of(const Walk& W, const Pt& pt, int i) {
 
 __device__ __forceinline__ bool odd_int(double v) { return v - 2.0 * floor(0.5 * v) != 0.0; }
 
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // a wave-uniform double into scalar registers
 __device__ __forceinline__ double uniform_f64(double v) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -611,9 +619,6 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
   int ib, ie;
   seg_bounds(W, pt, s, ib, ie);
   const int n = ie - ib;
-#ifdef FSCLG_EXP_NOPR
-  const uint32_t ex_p0 = P.pr[ib].x, ex_p1 = P.pr[max(ie - 1, ib)].x;
-#endif
   const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
   const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
   int civ = 0;
@@ -633,10 +638,7 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int k = kb + 64 * u + lane;
-#ifdef FSCLG_EXP_NOPR  // timing ablation only (wrong results): sites interpolated, no (position, row) load
-      const uint2 v = make_uint2(ex_p0 + (uint32_t)(((long long)(ex_p1 - ex_p0) * k) / (n > 0 ? n : 1)),
-                                 1u + (((uint32_t)(ib + k) * 2654435761u) >> 27));
-#elif !defined(FSCLG_NO_PF)
+#ifndef FSCLG_NO_PF
       const uint2 v = nx[u];
 #else
       const uint2 v = ld_pr(P.pr, (uint32_t)(ib + k));
@@ -644,33 +646,45 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
       pv[u] = v.x;
       rv[u] = (!MASK || k < n) ? v.y : 0u;  // zero sentinel row past the segment
     }
+    // log distance: when every lane's |d| lies in the LDS copy of the far branch (one
+    // unsigned compare per site: |d| in [2^24, lt_hi << 16)), straight from LDS; otherwise
+    // per lane (logt_lds).  Every lane is active in a trip, so the wave-wide tests below
+    // compare ballots with all ones.
     double x[U];
+    uint32_t ad[U];
+    bool far = true;
 #pragma unroll
-#ifdef FSCLG_EXP_LTLDS  // timing ablation only (wrong results): every log distance from the LDS table
-    for (int u = 0; u < U; u++)
-      x[u] = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt)[256 + ((absdist(pv[u], usweep) >> 16) % (uint32_t)(P.lt_hi - 256))] + la;
-#else
-    for (int u = 0; u < U; u++) x[u] = logt_lds<LDS>(absdist(pv[u], usweep), P) + la;
-#endif
+    for (int u = 0; u < U; u++) {
+      ad[u] = absdist(pv[u], usweep);
+      far = far && (ad[u] - 0x1000000u < (uint32_t)P.lt_span);
+    }
+    if (LDS && __builtin_amdgcn_ballot_w64(far) == ~0ull) {
+      const double* lt2 = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt);  // pre-offset by -256 entries
+#pragma unroll
+      for (int u = 0; u < U; u++) x[u] = lt2[ad[u] >> 16] + la;
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) x[u] = logt_lds<LDS>(ad[u], P) + la;
+    }
+    if (kb == 0) {  // a segment's first trip: centre the interval on its last site
+      const double xl = readlane_f64(x[U - 1], 63);
+      civ = __builtin_amdgcn_readfirstlane(interval_of<LDS>(xl, S, P));
+      tlo = uniform_f64(thrp[civ]);
+      thi = uniform_f64(thrp[civ + 1]);
+    }
     bool in = true;
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const bool ok = (x[u] >= tlo) && (x[u] < thi);
       in = in && (MASK ? (ok || kb + 64 * u + lane >= n) : ok);  // masked lanes add exactly 0 anyway
     }
+    const bool uni = __builtin_amdgcn_ballot_w64(in) == ~0ull;
     double2 ca[U], cb[U];
 #ifdef FSCLG_PATHSTATS  // diagnostic: trips per path in the stats slots 4 (per-lane), 5 (LDS), 6 (global)
-    const bool al = __all(in);
-    if (lane == 0) {
-      atomicAdd(&S.cnt[!al ? 4 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 5 : 6)], 1ull);
-    }
+    if (lane == 0) atomicAdd(&S.cnt[!uni ? 4 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 5 : 6)], 1ull);
 #endif
-    if (__all(in)) {
-#ifdef FSCLG_EXP_COEFLDS  // timing ablation only (wrong results): uniform trips always read the LDS window
-      const uint32_t ci = min((uint32_t)(civ - ivc0), (uint32_t)P.civ_max);
-#else
+    if (uni) {
       const uint32_t ci = (uint32_t)(civ - ivc0);
-#endif
       if (LDS && ci < (uint32_t)P.n_civ) {
         const char* lb = fsclg_dyn + (__umul24(ci, (uint32_t)P.stride) << 5);
 #pragma unroll
@@ -1771,6 +1785,7 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
   P.n_cache = P.n_civ * P.stride;
   P.off_thr = P.n_cache * 32; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
   P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8; P.lt_hi = c->lt_hi;  // entry i at off_lt + 8 i
+  P.lt_span = c->lt_hi > 256 ? ((uint32_t)c->lt_hi << 16) - 0x1000000u : 0u;  // lt_hi <= 32768
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null; P.win_null = c->d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
