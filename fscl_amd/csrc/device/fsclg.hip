@@ -672,13 +672,18 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
       tlo = uniform_f64(thrp[civ]);
       thi = uniform_f64(thrp[civ + 1]);
     }
-    bool in = true;
+    // one ballot per compare (SGPR masks, no bool materialised per lane)
+    unsigned long long inm = ~0ull;
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const bool ok = (x[u] >= tlo) && (x[u] < thi);
-      in = in && (MASK ? (ok || kb + 64 * u + lane >= n) : ok);  // masked lanes add exactly 0 anyway
+      if constexpr (MASK) {  // masked lanes add exactly 0 anyway
+        const bool ok = ((x[u] >= tlo) && (x[u] < thi)) || kb + 64 * u + lane >= n;
+        inm &= __builtin_amdgcn_ballot_w64(ok);
+      } else {
+        inm &= __builtin_amdgcn_ballot_w64(x[u] >= tlo) & __builtin_amdgcn_ballot_w64(x[u] < thi);
+      }
     }
-    const bool uni = __builtin_amdgcn_ballot_w64(in) == ~0ull;
+    const bool uni = inm == ~0ull;
     double2 ca[U], cb[U];
 #ifdef FSCLG_PATHSTATS  // diagnostic: trips per path in the stats slots 4 (per-lane), 5 (LDS), 6 (global)
     if (lane == 0) atomicAdd(&S.cnt[!uni ? 4 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 5 : 6)], 1ull);

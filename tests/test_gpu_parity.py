@@ -131,6 +131,24 @@ def test_shared_cells_and_endpoints_match_oracle(built, tmp):
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
 
 
+def test_tiny_chromosomes_match_oracle(built, tmp):
+    """Chromosomes of 1, 2, 3, 64, 65 and 130 SNPs among larger ones: the edges of the
+    wave-parallel searches (search_snppos over n = 1.., walk bounds over empty and
+    one-site sides) and windows that are the whole chromosome."""
+    chrs = []
+    for i, (k, length) in enumerate(((1, 50_000), (2, 90_000), (3, 150_000), (64, 700_000), (65, 900_000),
+                                     (130, 1_300_000), (3000, 3_000_000))):
+        chrs += synth.generate(n_chr=1, chr_len=length, snps_per_chr=k, n=16, seed=70 + i, chr_names=[f"t{i}"],
+                               sweeps_per_chr=1 if k >= 64 else 0)
+    snp = tmp / "tiny.snp"
+    synth.write_snp_file(str(snp), chrs)
+    opts = ["--coarse-grid-spacing=20000", "--n-permute=5"]
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), "tiny")
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+
+
 def test_ms_input_matches_oracle_on_converted_file(built, tmp):
     ms = tmp / "x.ms"
     synth.write_ms_file(str(ms), n_blocks=4, n_hap=20, n_seg=600, seed=41)
