@@ -78,7 +78,8 @@ class Stats(C.Structure):  # fscl_amd_stats_t
                 ("cache_iv0", C.c_int), ("cache_n_iv", C.c_int), ("cache_n_rows", C.c_int),
                 ("cache_cover", C.c_double), ("window_ms", C.c_double), ("host_null_s", C.c_double),
                 ("host_upload_s", C.c_double), ("search_s", C.c_double), ("prune_s", C.c_double),
-                ("n_dup_cells", C.c_ulonglong), ("n_ep_saved", C.c_ulonglong)]
+                ("n_dup_cells", C.c_ulonglong), ("n_ep_saved", C.c_ulonglong), ("busy_ms", C.c_double),
+                ("wait_s", C.c_double), ("n_crit", C.c_ulonglong), ("n_drain", C.c_ulonglong)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -96,6 +97,7 @@ EXPORTS = [
     "fsclg_open", "fsclg_close", "fsclg_last_error", "fsclg_device_count", "fsclg_upload_tables",
     "fsclg_upload_snps", "fsclg_set_rows", "fsclg_set_chr_null", "fsclg_set_alpha_grid", "fsclg_search_maxpos",
     "fsclg_search_points", "fsclg_get_stats", "fsclg_reset_stats", "fsclg_interval_thresholds",
+    "fsclg_row_buffer", "fsclg_slot_row_buffer", "fsclg_slot_set_rows", "fsclg_search_submit", "fsclg_search_wait",
 ]
 
 

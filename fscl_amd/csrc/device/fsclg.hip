@@ -1227,11 +1227,13 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
       }
       __syncthreads();
     }
-    if (tid == 0) {
+    if (tid == 0) {  // one store of the result (P.out may be host memory: no read-modify-write)
       const Pt& r = S.pt[0].clr > S.pt[1].clr ? S.pt[0] : S.pt[1];
-      write_point(P.out[cell], r);
-      P.out[cell].flags |= S.pt[0].flags | S.pt[1].flags;
-      P.out[cell].cost = (uint32_t)min(S.cnt[0] >> 10, 0xFFFFFFFFull);
+      fsclg_point_t o;
+      write_point(o, r);
+      o.flags |= S.pt[0].flags | S.pt[1].flags;
+      o.cost = (uint32_t)min(S.cnt[0] >> 10, 0xFFFFFFFFull);
+      P.out[cell] = o;
       S.cnt[7] += 1;
     }
   }
@@ -1295,20 +1297,75 @@ __global__ void __launch_bounds__(WN_WG) window_null_kernel(const uint2* __restr
   if (nwin > 3) out[base + 3] = a3;
 }
 
-// one trial's rows into the (position, row) array: pr[i].y = row[i] + 1 (device row)
+// one trial's rows into the (position, row) array: pr[i].y = row[i] + 1 (device row), read
+// straight from the pinned host staging (no copy-engine transfer, which would order this
+// stream's work behind other streams' copies); block 0 also takes the whole-chromosome null
+// sums.  row == null: the uploaded rows (pr0).
 __global__ void __launch_bounds__(256) scatter_rows_kernel(uint2* __restrict__ pr, const uint32_t* __restrict__ row,
-                                                           int n) {
+                                                           const uint2* __restrict__ pr0, int n,
+                                                           double* __restrict__ chr_null,
+                                                           const double* __restrict__ chr_null_src, int n_chr) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) pr[i].y = row[i] + 1u;
+  if (i < n) pr[i].y = row ? row[i] + 1u : pr0[i].y;
+  if (blockIdx.x == 0 && chr_null_src)
+    for (int c = threadIdx.x; c < n_chr; c += 256) chr_null[c] = chr_null_src[c];
 }
 
 }  // namespace
 
 // ----------------------------------------------------------------- host shim
+constexpr int NSLOT = FSCLG_N_SLOTS;
+constexpr int NBATCH = FSCLG_N_BATCHES;
+
+// one trial's rows on the device (fsclg_slot_set_rows): the (position, row) array, the
+// whole-chromosome null sums and the per-window null sums of those rows
+struct Slot {
+  uint2* d_pr = nullptr;          // (biased position, device row), n_snps + PAD
+  double* d_chr_null = nullptr;
+  double* d_win_null = nullptr;   // [n_snps], valid for (win_er, rows) while win_valid
+  int win_er = -1;
+  bool win_valid = false;
+  uint32_t* h_rows = nullptr;     // pinned (coherent) staging of one trial's rows, read by scatter_rows_kernel
+  double* h_null = nullptr;       // pinned (coherent) whole-chromosome null sums, n_chr
+  int rows_cap = 0, null_cap = 0;
+  hipEvent_t ready = nullptr;     // recorded on the upload stream after the slot's last upload
+  int users = 0;                  // batches submitted on this slot and not yet waited for
+};
+
+// one search_maxpos launch group (fsclg_search_submit / fsclg_search_wait): its stream,
+// events, device and pinned host buffers, and the host-side dedup / ordering of its cells
+struct Batch {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // bracket the kernels
+  hipEvent_t ev2 = nullptr;                  // after the results' D2H
+  // the kernels read their inputs from and write their outputs to pinned coherent host memory
+  // (a few bytes per workgroup): no copy-engine transfers on the batch streams, which would
+  // order one stream's kernels behind another stream's copies and serialise the trials
+  fsclg_cell_t* p_cells = nullptr;
+  fsclg_point_t* p_out = nullptr;
+  int cap = 0;
+  fsclg_point_t* d_ept = nullptr;   // endpoint results: written by one launch, read by the next
+  int2* p_epos = nullptr;
+  int2* p_cell_ep = nullptr;
+  int ept_cap = 0, pep_cap = 0, pcep_cap = 0;
+  unsigned long long* p_ctrace = nullptr;  // FSCLG_CELL_TRACE=<file>: per-cell timing appended per launch
+  int ctrace_cap = 0;
+  unsigned long long* ivhist = nullptr;    // this launch measures the interval histogram (FSCLG_IVHIST)
+  bool traced = false;
+  std::unordered_map<unsigned long long, int> umap, emap;
+  std::vector<int> uidx, upos, order;
+  std::vector<fsclg_cell_t> ucells;
+  std::vector<int2> epos, ucell_ep;
+  int n_cells = 0, nu = 0, nlaunch = 0, slot = -1;
+  bool pending = false;
+};
+
 struct fsclg_ctx {
   int device;
-  hipStream_t stream;
-  hipEvent_t ev0, ev1;
+  hipStream_t ustream;            // uploads (rows, null sums, window sums), high priority
+  hipStream_t bstream[3];         // batches 0-1: high priority; even / odd batches 2..: normal
+  hipEvent_t ev_ref;              // time origin of the busy intervals (fsclg_reset_stats)
+  hipEvent_t wev0, wev1;          // window null-sum kernel timing
   // tables
   double* d_logt = nullptr;
   double* d_coef = nullptr;
@@ -1317,21 +1374,17 @@ struct fsclg_ctx {
   int n_rows = 0, n_iv = 0;
   double step = 0.0;
   // snps
-  uint2* d_pr = nullptr;          // (biased position, device row), n_snps + PAD
-  uint2* d_pr0 = nullptr;         // the same with the unpermuted rows
+  uint2* d_pr0 = nullptr;         // (biased position, device row) with the unpermuted rows
   std::vector<uint2> h_pr0;
-  uint2* d_prs = nullptr;         // row-sorted BLK-blocks of d_pr (null: rows too many for 16 bits)
+  uint2* d_prs = nullptr;         // row-sorted BLK-blocks of slot 0's rows (null: no sorted path)
   uint2* d_prs0 = nullptr;
   std::vector<uint2> h_prs;
   std::vector<int> h_cnt;
   int n_snps = 0;
   int32_t* d_chr_start = nullptr;
   int32_t* d_chr_n = nullptr;
-  double* d_chr_null = nullptr;
-  double* d_win_null = nullptr;           // [n_snps], valid for (win_er, rows) while win_valid
   int2* d_wtasks = nullptr;
-  int n_wtasks = 0, wtask_cap = 0, win_er = -1;
-  bool win_valid = false;
+  int n_wtasks = 0, wtask_cap = 0, wtask_er = -1;
   double window_ms = 0.0;
   int n_chr = 0;
   std::vector<int> h_chr_n;
@@ -1340,9 +1393,8 @@ struct fsclg_ctx {
   std::vector<long long> h_row_cnt;     // sites per device row
   std::vector<double> h_lt3;
   std::vector<uint2> h_stage;
-  uint32_t* h_rows = nullptr;     // pinned staging of one trial's rows
-  uint32_t* d_rows = nullptr;
-  int rows_cap = 0;
+  Slot slot[NSLOT];
+  Batch batch[NBATCH];
   // LDS coefficient cache plan (fsclg_plan_cache)
   bool plan_dirty = true;
   bool hist_pending = false;          // the next search_maxpos launch measures the interval histogram
@@ -1357,29 +1409,12 @@ struct fsclg_ctx {
   double* d_la_refine = nullptr;
   int32_t* d_n_refine = nullptr;
   int n_coarse = 0;
-  // io
-  fsclg_cell_t* d_cells = nullptr;
-  fsclg_point_t* d_out = nullptr;
-  int cap = 0;
   unsigned long long* d_stats = nullptr;
   std::unordered_map<unsigned long long, uint32_t> cell_cost;  // (chr, start, end) -> cost of its last run
-  std::vector<fsclg_cell_t> h_cells;
-  std::vector<int> h_order;
-  std::vector<fsclg_point_t> h_out;
-  // cell / endpoint deduplication
-  std::unordered_map<unsigned long long, int> h_umap, h_emap;
-  std::vector<int> h_uidx, h_upos;
-  std::vector<fsclg_cell_t> h_ucells;
-  std::vector<int2> h_epos, h_cell_ep, h_ucell_ep;
-  int2* d_epos = nullptr;
-  int2* d_cell_ep = nullptr;
-  fsclg_point_t* d_ept = nullptr;
-  int epos_cap = 0, cell_ep_cap = 0, ept_cap = 0;
   unsigned long long n_dup_cells = 0, n_ep_saved = 0;
-  unsigned long long* d_ctrace = nullptr;  // FSCLG_CELL_TRACE=<file>: per-cell timing appended per launch
-  int ctrace_cap = 0;
   double kernel_ms = 0.0;
   unsigned long long launches = 0;
+  std::vector<std::pair<double, double>> busy;  // [start, end) ms of each batch's kernels since ev_ref
 };
 
 static thread_local char g_err[512];
@@ -1457,11 +1492,28 @@ int fsclg_open(int device, fsclg_ctx** out) {
   HIPCHK(hipSetDevice(device), "hipSetDevice");
   fsclg_ctx* c = new fsclg_ctx();
   c->device = device;
-  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
-  HIPCHK(hipEventCreate(&c->ev0), "hipEventCreate");
-  HIPCHK(hipEventCreate(&c->ev1), "hipEventCreate");
+  // the rand-stream critical batches (and the uploads they wait for) get the high-priority
+  // streams: their workgroups take the next free slots ahead of the bulk of a trial
+  int lo = 0, hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+  HIPCHK(hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, hi), "hipStreamCreate");
+  for (int k = 0; k < 3; k++)
+    HIPCHK(hipStreamCreateWithPriority(&c->bstream[k], hipStreamNonBlocking, k == 0 ? hi : lo), "hipStreamCreate");
+  for (int b = 0; b < NBATCH; b++) {
+    Batch& B = c->batch[b];
+    B.stream = c->bstream[b < 2 ? 0 : 1 + (b & 1)];
+    HIPCHK(hipEventCreate(&B.ev0), "hipEventCreate");
+    HIPCHK(hipEventCreate(&B.ev1), "hipEventCreate");
+    HIPCHK(hipEventCreateWithFlags(&B.ev2, hipEventDisableTiming), "hipEventCreate");
+  }
+  for (int s = 0; s < NSLOT; s++) HIPCHK(hipEventCreateWithFlags(&c->slot[s].ready, hipEventDisableTiming), "hipEventCreate");
+  HIPCHK(hipEventCreate(&c->ev_ref), "hipEventCreate");
+  HIPCHK(hipEventCreate(&c->wev0), "hipEventCreate");
+  HIPCHK(hipEventCreate(&c->wev1), "hipEventCreate");
   HIPCHK(hipMalloc((void**)&c->d_stats, sizeof(unsigned long long) * 8), "hipMalloc stats");
   HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
+  HIPCHK(hipEventRecord(c->ev_ref, c->ustream), "hipEventRecord");
+  HIPCHK(hipEventSynchronize(c->ev_ref), "hipEventSynchronize");
   *out = c;
   return FSCLG_OK;
 }
@@ -1469,17 +1521,36 @@ int fsclg_open(int device, fsclg_ctx** out) {
 int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
   hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_ctrace, c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr, c->d_pr0, c->d_prs, c->d_prs0, c->d_chr_start, c->d_chr_n,
-                  c->d_chr_null, c->d_win_null, c->d_wtasks, c->d_epos, c->d_cell_ep, c->d_ept, c->d_la_coarse, c->d_la_refine, c->d_n_refine, c->d_cells, c->d_out, c->d_stats};
+  hipDeviceSynchronize();
+  void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0, c->d_prs, c->d_prs0,
+                  c->d_chr_start, c->d_chr_n, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine,
+                  c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
-  if (c->d_rows) hipFree(c->d_rows);
-  if (c->h_rows) hipHostFree(c->h_rows);
-  hipEventDestroy(c->ev0);
-  hipEventDestroy(c->ev1);
-  hipStreamDestroy(c->stream);
+  for (Slot& S : c->slot) {
+    for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null}) if (p) hipFree(p);
+    for (void* p : {(void*)S.h_rows, (void*)S.h_null}) if (p) hipHostFree(p);
+    hipEventDestroy(S.ready);
+  }
+  for (Batch& B : c->batch) {
+    if (B.d_ept) hipFree(B.d_ept);
+    for (void* p : {(void*)B.p_cells, (void*)B.p_out, (void*)B.p_epos, (void*)B.p_cell_ep, (void*)B.p_ctrace})
+      if (p) hipHostFree(p);
+    hipEventDestroy(B.ev0);
+    hipEventDestroy(B.ev1);
+    hipEventDestroy(B.ev2);
+  }
+  for (hipStream_t st : c->bstream) hipStreamDestroy(st);
+  hipEventDestroy(c->ev_ref);
+  hipEventDestroy(c->wev0);
+  hipEventDestroy(c->wev1);
+  hipStreamDestroy(c->ustream);
   delete c;
   return FSCLG_OK;
+}
+
+static bool any_pending(const fsclg_ctx* c) {
+  for (const Batch& B : c->batch) if (B.pending) return true;
+  return false;
 }
 
 int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coef, int n_rows, int n_iv,
@@ -1487,6 +1558,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   if (!c || !log_table || !coef || !nullrow || n_rows <= 0 || n_iv <= 0) return set_err(FSCLG_E_ARG, "tables");
   if ((unsigned long long)(n_rows + 1) * (unsigned long long)n_iv * 32ull >= (1ull << 32))
     return set_err(FSCLG_E_ARG, "coefficient table exceeds 4 GiB (32-bit offsets)");
+  if (any_pending(c)) return set_err(FSCLG_E_STATE, "search batches in flight");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
   // the three branches of sm-search.c:40-46 (c_b + log_table[i]) as one table; the same
@@ -1498,7 +1570,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
       volatile double v = cb[b] + log_table[i];
       lt3[(size_t)b * 0x10000 + i] = b ? (double)v : log_table[i];
     }
-  if ((r = upload(&c->d_logt, lt3.data(), lt3.size(), c->stream))) return r;
+  if ((r = upload(&c->d_logt, lt3.data(), lt3.size(), c->ustream))) return r;
   c->h_lt3.swap(lt3);
   // [row][iv][4] -> [iv][plane][1 + row][2] (coef_off): device row 0 is an all-zero sentinel
   // (terms exactly 0); plane 0 holds (c0, c1), plane 1 (c2, c3)
@@ -1509,24 +1581,25 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
       for (int pl = 0; pl < 2; pl++)
         memcpy(&tcoef[(((size_t)iv * 2 + pl) * stride + rr + 1) * 2], coef + ((size_t)rr * n_iv + iv) * 4 + 2 * pl,
                sizeof(double) * 2);
-  if ((r = upload(&c->d_coef, tcoef.data(), tcoef.size(), c->stream))) return r;
+  if ((r = upload(&c->d_coef, tcoef.data(), tcoef.size(), c->ustream))) return r;
   std::vector<double> nul(1, 0.0);
   nul.insert(nul.end(), nullrow, nullrow + n_rows);
-  if ((r = upload(&c->d_null, nul.data(), nul.size(), c->stream))) return r;
+  if ((r = upload(&c->d_null, nul.data(), nul.size(), c->ustream))) return r;
   std::vector<double> thr((size_t)n_iv + 1, 0.0);
   for (int j = 1; j < n_iv; j++) thr[j] = interval_threshold(j, log_ad_step);
   thr[0] = -__builtin_inf();     // iv 0 never steps down
   thr[n_iv] = __builtin_inf();   // iv n_iv-1 never steps up (the reference clamps)
-  if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->stream))) return r;
+  if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->ustream))) return r;
   c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
   c->plan_dirty = true;
-  c->win_valid = false;
+  for (Slot& S : c->slot) S.win_valid = false;
   return FSCLG_OK;
 }
 
 int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int n_snps,
                       const int32_t* chr_start, const int32_t* chr_n, int n_chr) {
   if (!c || !pos || !row || n_snps <= 0 || !chr_start || !chr_n || n_chr <= 0) return set_err(FSCLG_E_ARG, "snps");
+  if (any_pending(c)) return set_err(FSCLG_E_STATE, "search batches in flight");
   for (int i = 0; i < n_chr; i++)
     if (chr_start[i] < 0 || chr_n[i] <= 0 || chr_start[i] + chr_n[i] > n_snps) return set_err(FSCLG_E_ARG, "chr limits");
   for (int i = 0; i < n_snps; i++)
@@ -1536,12 +1609,18 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   // PAD slack after both arrays (zeros: a valid position and row, never counted)
   std::vector<uint2> pr((size_t)n_snps + PAD, make_uint2(POS_BIAS, 0u));
   for (int i = 0; i < n_snps; i++) pr[i] = make_uint2((uint32_t)pos[i] ^ POS_BIAS, row[i] + 1);
-  if ((r = upload(&c->d_pr0, pr.data(), pr.size(), c->stream))) return r;
-  if ((r = upload(&c->d_pr, pr.data(), pr.size(), c->stream))) return r;
+  if ((r = upload(&c->d_pr0, pr.data(), pr.size(), c->ustream))) return r;
+  for (Slot& S : c->slot) {
+    if ((r = upload(&S.d_pr, pr.data(), pr.size(), c->ustream))) return r;
+    if ((r = upload<double>(&S.d_chr_null, nullptr, (size_t)n_chr, c->ustream))) return r;
+    if ((r = upload<double>(&S.d_win_null, nullptr, (size_t)n_snps, c->ustream))) return r;
+    S.win_valid = false; S.win_er = -1;
+    HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
+  }
   c->n_snps = n_snps;
   // row-sorted blocks: fewer cache lines per coefficient gather, but measured slower once the
   // coefficient windows follow the walks (the texture data path is bound by bytes, not
-  // lines); kept as an option (FSCLG_SORTED=1), parity-tested
+  // lines); kept as an option for slot 0 (FSCLG_SORTED=1), parity-tested
 #ifdef FSCLG_SORTED_PATH
   const bool sorted_path = true;
 #else
@@ -1549,18 +1628,16 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
 #endif
   if (sorted_path && c->n_rows > 0 && c->n_rows + 1 < 0x10000 && getenv("FSCLG_SORTED")) {
     sort_blocks(c, pr.data());
-    if ((r = upload(&c->d_prs0, c->h_prs.data(), c->h_prs.size(), c->stream))) return r;
-    if ((r = upload(&c->d_prs, c->h_prs.data(), c->h_prs.size(), c->stream))) return r;
+    if ((r = upload(&c->d_prs0, c->h_prs.data(), c->h_prs.size(), c->ustream))) return r;
+    if ((r = upload(&c->d_prs, c->h_prs.data(), c->h_prs.size(), c->ustream))) return r;
   } else {
     if (c->d_prs) hipFree(c->d_prs);
     if (c->d_prs0) hipFree(c->d_prs0);
     c->d_prs = nullptr; c->d_prs0 = nullptr;
   }
-  if ((r = upload(&c->d_chr_start, chr_start, (size_t)n_chr, c->stream))) return r;
-  if ((r = upload(&c->d_chr_n, chr_n, (size_t)n_chr, c->stream))) return r;
-  if ((r = upload<double>(&c->d_chr_null, nullptr, (size_t)n_chr, c->stream))) return r;
-  if ((r = upload<double>(&c->d_win_null, nullptr, (size_t)n_snps, c->stream))) return r;
-  c->win_valid = false; c->win_er = -1;
+  if ((r = upload(&c->d_chr_start, chr_start, (size_t)n_chr, c->ustream))) return r;
+  if ((r = upload(&c->d_chr_n, chr_n, (size_t)n_chr, c->ustream))) return r;
+  c->wtask_er = -1;
   c->n_snps = n_snps; c->n_chr = n_chr;
   c->h_chr_n.assign(chr_n, chr_n + n_chr);
   c->h_chr_start.assign(chr_start, chr_start + n_chr);
@@ -1583,61 +1660,92 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   return FSCLG_OK;
 }
 
-static int ensure_row_staging(fsclg_ctx* c) {
-  if (c->rows_cap >= c->n_snps) return FSCLG_OK;
-  if (c->h_rows) hipHostFree(c->h_rows);
-  if (c->d_rows) hipFree(c->d_rows);
-  c->h_rows = nullptr; c->d_rows = nullptr; c->rows_cap = 0;
-  HIPCHK(hipHostMalloc((void**)&c->h_rows, sizeof(uint32_t) * c->n_snps, hipHostMallocDefault), "hipHostMalloc rows");
-  HIPCHK(hipMalloc((void**)&c->d_rows, sizeof(uint32_t) * c->n_snps), "hipMalloc rows");
-  c->rows_cap = c->n_snps;
+// pinned host memory the kernels read or write directly (coherent: no cache flush needed
+// between a kernel's stores and the host's reads after its completion event)
+static constexpr unsigned HOSTMEM = hipHostMallocCoherent | hipHostMallocMapped;
+
+static int ensure_row_staging(fsclg_ctx* c, Slot& S) {
+  if (S.null_cap < c->n_chr) {
+    if (S.h_null) hipHostFree(S.h_null);
+    S.h_null = nullptr; S.null_cap = 0;
+    HIPCHK(hipHostMalloc((void**)&S.h_null, sizeof(double) * c->n_chr, HOSTMEM), "hipHostMalloc null sums");
+    S.null_cap = c->n_chr;
+  }
+  if (S.rows_cap >= c->n_snps) return FSCLG_OK;
+  if (S.h_rows) hipHostFree(S.h_rows);
+  S.h_rows = nullptr; S.rows_cap = 0;
+  HIPCHK(hipHostMalloc((void**)&S.h_rows, sizeof(uint32_t) * c->n_snps, HOSTMEM), "hipHostMalloc rows");
+  S.rows_cap = c->n_snps;
   return FSCLG_OK;
 }
 
-uint32_t* fsclg_row_buffer(fsclg_ctx* c) {
-  if (!c || !c->d_pr) { set_err(FSCLG_E_STATE, "snps not uploaded"); return nullptr; }
-  if (hipSetDevice(c->device) != hipSuccess || ensure_row_staging(c) != FSCLG_OK) return nullptr;
-  return c->h_rows;
+uint32_t* fsclg_slot_row_buffer(fsclg_ctx* c, int slot) {
+  if (!c || !c->d_pr0) { set_err(FSCLG_E_STATE, "snps not uploaded"); return nullptr; }
+  if (slot < 0 || slot >= NSLOT) { set_err(FSCLG_E_ARG, "slot"); return nullptr; }
+  Slot& S = c->slot[slot];
+  if (S.users) { set_err(FSCLG_E_STATE, "slot in use by a batch not waited for"); return nullptr; }
+  if (hipSetDevice(c->device) != hipSuccess || ensure_row_staging(c, S) != FSCLG_OK) return nullptr;
+  // the slot's last upload may still read the buffer
+  if (hipEventSynchronize(S.ready) != hipSuccess) { set_err(FSCLG_E_HIP, "hipEventSynchronize"); return nullptr; }
+  return S.h_rows;
 }
 
-int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) {
-  if (!c || !c->d_pr) return set_err(FSCLG_E_STATE, "snps not uploaded");
+uint32_t* fsclg_row_buffer(fsclg_ctx* c) { return fsclg_slot_row_buffer(c, 0); }
+
+int fsclg_slot_set_rows(fsclg_ctx* c, int slot, const uint32_t* row, const double* chr_null) {
+  if (!c || !c->d_pr0) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  if (slot < 0 || slot >= NSLOT) return set_err(FSCLG_E_ARG, "slot");
+  Slot& S = c->slot[slot];
+  if (S.users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
-  c->win_valid = false;
-  if (!row) {
-    HIPCHK(hipMemcpyAsync(c->d_pr, c->d_pr0, sizeof(uint2) * c->n_snps, hipMemcpyDeviceToDevice, c->stream), "copy rows");
-    if (c->d_prs)
-      HIPCHK(hipMemcpyAsync(c->d_prs, c->d_prs0, sizeof(uint2) * c->h_prs.size(), hipMemcpyDeviceToDevice, c->stream),
-             "copy sorted rows");
-  } else {
+  int r;
+  if ((r = ensure_row_staging(c, S))) return r;
+  HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read the staging
+  S.win_valid = false;
+  if (row) {
     uint32_t mx = 0;
     for (int i = 0; i < c->n_snps; i++) mx = row[i] > mx ? row[i] : mx;  // vectorised validation
     if (mx >= (uint32_t)c->n_rows) return set_err(FSCLG_E_ARG, "row index out of table");
-    int r;
-    if ((r = ensure_row_staging(c))) return r;
-    // the previous trial's copy has completed (its search synchronised the stream)
-    if (row != c->h_rows) memcpy(c->h_rows, row, sizeof(uint32_t) * c->n_snps);
-    HIPCHK(hipMemcpyAsync(c->d_rows, c->h_rows, sizeof(uint32_t) * c->n_snps, hipMemcpyHostToDevice, c->stream),
-           "copy rows");
-    hipLaunchKernelGGL(scatter_rows_kernel, dim3((c->n_snps + 255) / 256), dim3(256), 0, c->stream, c->d_pr,
-                       c->d_rows, c->n_snps);
-    HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
-    if (c->d_prs) {  // opt-in row-sorted blocks: built on the host
+    if (row != S.h_rows) memcpy(S.h_rows, row, sizeof(uint32_t) * c->n_snps);
+  }
+  if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((c->n_snps + 255) / 256), dim3(256), 0, c->ustream, S.d_pr,
+                     row ? S.h_rows : nullptr, c->d_pr0, c->n_snps, S.d_chr_null, chr_null ? S.h_null : nullptr,
+                     c->n_chr);
+  HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
+  if (c->d_prs && slot == 0) {  // opt-in row-sorted blocks (diagnostic): built on the host
+    if (!row) {
+      HIPCHK(hipMemcpyAsync(c->d_prs, c->d_prs0, sizeof(uint2) * c->h_prs.size(), hipMemcpyDeviceToDevice, c->ustream),
+             "copy sorted rows");
+    } else {
       c->h_stage.resize(c->n_snps);
       for (int i = 0; i < c->n_snps; i++) c->h_stage[i] = make_uint2(c->h_pr0[i].x, row[i] + 1);
       sort_blocks(c, c->h_stage.data());
-      HIPCHK(hipMemcpyAsync(c->d_prs, c->h_prs.data(), sizeof(uint2) * c->h_prs.size(), hipMemcpyHostToDevice, c->stream),
+      HIPCHK(hipMemcpyAsync(c->d_prs, c->h_prs.data(), sizeof(uint2) * c->h_prs.size(), hipMemcpyHostToDevice, c->ustream),
              "copy sorted rows");
-      HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");  // h_prs is reused
     }
+    HIPCHK(hipStreamSynchronize(c->ustream), "hipStreamSynchronize");  // h_prs is reused
   }
+  HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   return FSCLG_OK;
 }
 
+int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) { return fsclg_slot_set_rows(c, 0, row, nullptr); }
+
 int fsclg_set_chr_null(fsclg_ctx* c, const double* chr_null) {
-  if (!c || !c->d_chr_null || !chr_null) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  if (!c || !c->d_pr0 || !chr_null) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  Slot& S = c->slot[0];
+  if (S.users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
-  HIPCHK(hipMemcpyAsync(c->d_chr_null, chr_null, sizeof(double) * c->n_chr, hipMemcpyHostToDevice, c->stream), "copy null");
+  int r;
+  if ((r = ensure_row_staging(c, S))) return r;
+  HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");
+  memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
+  // the null sums only: a one-block scatter over no sites
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(1), dim3(256), 0, c->ustream, S.d_pr, nullptr, c->d_pr0, 0,
+                     S.d_chr_null, S.h_null, c->n_chr);
+  HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
+  HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   return FSCLG_OK;
 }
 
@@ -1650,11 +1758,12 @@ int fsclg_set_alpha_grid(fsclg_ctx* c, const double* coarse, int n_coarse, const
   for (int i = 0; i <= n_coarse; i++)
     for (int r = 0; r < n_refine[i]; r++)
       if (!(refine[i * MAXREF + r] >= LOG_AD_MIN)) return set_err(FSCLG_E_ARG, "alpha below LOG_AD_MIN");
+  if (any_pending(c)) return set_err(FSCLG_E_STATE, "search batches in flight");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
-  if ((r = upload(&c->d_la_coarse, coarse, (size_t)n_coarse, c->stream))) return r;
-  if ((r = upload(&c->d_la_refine, refine, (size_t)(n_coarse + 1) * MAXREF, c->stream))) return r;
-  if ((r = upload(&c->d_n_refine, n_refine, (size_t)(n_coarse + 1), c->stream))) return r;
+  if ((r = upload(&c->d_la_coarse, coarse, (size_t)n_coarse, c->ustream))) return r;
+  if ((r = upload(&c->d_la_refine, refine, (size_t)(n_coarse + 1) * MAXREF, c->ustream))) return r;
+  if ((r = upload(&c->d_n_refine, n_refine, (size_t)(n_coarse + 1), c->ustream))) return r;
   c->n_coarse = n_coarse;
   c->h_coarse.assign(coarse, coarse + n_coarse);
   c->h_refine.assign(refine, refine + (size_t)(n_coarse + 1) * MAXREF);
@@ -1663,24 +1772,24 @@ int fsclg_set_alpha_grid(fsclg_ctx* c, const double* coarse, int n_coarse, const
   return FSCLG_OK;
 }
 
-static int ensure_io(fsclg_ctx* c, int n) {
-  if (n <= c->cap) return FSCLG_OK;
-  if (c->d_cells) hipFree(c->d_cells);
-  if (c->d_out) hipFree(c->d_out);
-  c->d_cells = nullptr; c->d_out = nullptr;
-  int cap = n < 1024 ? 1024 : n;
-  HIPCHK(hipMalloc((void**)&c->d_cells, sizeof(fsclg_cell_t) * cap), "hipMalloc cells");
-  HIPCHK(hipMalloc((void**)&c->d_out, sizeof(fsclg_point_t) * cap), "hipMalloc out");
-  c->cap = cap;
+static int ensure_io(Batch& B, int n) {
+  if (n <= B.cap) return FSCLG_OK;
+  for (void* p : {(void*)B.p_cells, (void*)B.p_out}) if (p) hipHostFree(p);
+  B.p_cells = nullptr; B.p_out = nullptr; B.cap = 0;
+  const int cap = n < 1024 ? 1024 : n;
+  HIPCHK(hipHostMalloc((void**)&B.p_cells, sizeof(fsclg_cell_t) * cap, HOSTMEM), "hipHostMalloc cells");
+  HIPCHK(hipHostMalloc((void**)&B.p_out, sizeof(fsclg_point_t) * cap, HOSTMEM), "hipHostMalloc out");
+  B.cap = cap;
   return FSCLG_OK;
 }
 
-// the null sums of every window of the chromosomes longer than 2*er+1 SNPs, for the
-// current rows (window_null_kernel, on the search stream, timed apart from the search)
-static int ensure_windows(fsclg_ctx* c, int er) {
+// the null sums of every window of the chromosomes longer than 2*er+1 SNPs, for the slot's
+// rows (window_null_kernel on the upload stream, timed apart from the search)
+static int ensure_windows(fsclg_ctx* c, int slot, int er) {
   const long long W = 2ll * er + 1;
-  if (c->win_valid && c->win_er == er) return FSCLG_OK;
-  if (c->win_er != er) {
+  Slot& S = c->slot[slot];
+  if (S.win_valid && S.win_er == er) return FSCLG_OK;
+  if (c->wtask_er != er) {
     std::vector<int2> tasks;
     for (int ch = 0; ch < c->n_chr; ch++) {
       const long long n = c->h_chr_n[ch];
@@ -1689,6 +1798,9 @@ static int ensure_windows(fsclg_ctx* c, int er) {
       for (int o = 0; o < cnt; o += WN_WG * WN_PER)
         tasks.push_back(make_int2(c->h_chr_start[ch] + o, std::min(WN_WG * WN_PER, cnt - o)));
     }
+    // every launch reading the task list has completed (no batch runs on a slot being set up;
+    // the other slot's window launch ran on this same stream)
+    HIPCHK(hipStreamSynchronize(c->ustream), "hipStreamSynchronize");
     c->n_wtasks = (int)tasks.size();
     if (c->n_wtasks > c->wtask_cap) {
       if (c->d_wtasks) hipFree(c->d_wtasks);
@@ -1697,25 +1809,28 @@ static int ensure_windows(fsclg_ctx* c, int er) {
       c->wtask_cap = c->n_wtasks;
     }
     if (c->n_wtasks)
-      HIPCHK(hipMemcpyAsync(c->d_wtasks, tasks.data(), sizeof(int2) * tasks.size(), hipMemcpyHostToDevice, c->stream),
+      HIPCHK(hipMemcpyAsync(c->d_wtasks, tasks.data(), sizeof(int2) * tasks.size(), hipMemcpyHostToDevice, c->ustream),
              "copy window tasks");
-    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
-    c->win_er = er;
+    HIPCHK(hipStreamSynchronize(c->ustream), "hipStreamSynchronize");
+    c->wtask_er = er;
   }
   if (c->n_wtasks) {
-    HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
-    hipLaunchKernelGGL(window_null_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->stream, c->d_pr, c->d_null,
-                       c->d_wtasks, (int)W, c->d_win_null);
+    HIPCHK(hipEventRecord(c->wev0, c->ustream), "hipEventRecord");
+    hipLaunchKernelGGL(window_null_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
+                       c->d_wtasks, (int)W, S.d_win_null);
     HIPCHK(hipGetLastError(), "launch window_null_kernel");
-    HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
-    HIPCHK(hipEventSynchronize(c->ev1), "hipEventSynchronize");
+    HIPCHK(hipEventRecord(c->wev1, c->ustream), "hipEventRecord");
+    HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
+    HIPCHK(hipEventSynchronize(c->wev1), "hipEventSynchronize");
     float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
+    HIPCHK(hipEventElapsedTime(&ms, c->wev0, c->wev1), "hipEventElapsedTime");
     c->window_ms += ms;
   }
-  c->win_valid = true;
+  S.win_er = er;
+  S.win_valid = true;
   return FSCLG_OK;
 }
+
 
 // the best window of K = room / (rows * 32) intervals for a histogram of terms per interval.
 // Every row is held: a miss sends the whole wave's gather to the global table, so a row
@@ -1779,9 +1894,10 @@ static void plan_cache(fsclg_ctx* c) {
 #endif
 }
 
-static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_resl) {
+static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int eval_range, int bp_resl) {
+  const Slot& S = c->slot[slot];
   Params P;
-  P.pr = c->d_pr; P.prs = c->d_prs; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
+  P.pr = S.d_pr; P.prs = slot == 0 ? c->d_prs : nullptr; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
   P.thr = c->d_thr; P.n_rows = c->n_rows; P.stride = c->n_rows + 1; P.pstride = P.stride * 16;
   P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step - 1e-9;
   // dynamic LDS: the planned coefficient window, thresholds and null rows
@@ -1791,25 +1907,25 @@ static Params make_params(fsclg_ctx* c, int n, int mode, int eval_range, int bp_
   P.off_thr = P.n_cache * 32; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
   P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8; P.lt_hi = c->lt_hi;  // entry i at off_lt + 8 i
   P.lt_span = c->lt_hi > 256 ? ((uint32_t)c->lt_hi << 16) - 0x1000000u : 0u;  // lt_hi <= 32768
-  P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = c->d_chr_null; P.win_null = c->d_win_null;
+  P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = S.d_chr_null; P.win_null = S.d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
-  P.cells = c->d_cells; P.out = c->d_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
+  P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
   if (getenv("FSCLG_CELL_TRACE")) {
-    if (c->ctrace_cap < n) {
-      if (c->d_ctrace) hipFree(c->d_ctrace);
-      c->d_ctrace = nullptr;
-      if (hipMalloc((void**)&c->d_ctrace, sizeof(unsigned long long) * 8 * n) == hipSuccess) c->ctrace_cap = n;
+    if (B.ctrace_cap < n) {
+      if (B.p_ctrace) hipHostFree(B.p_ctrace);
+      B.p_ctrace = nullptr; B.ctrace_cap = 0;
+      if (hipHostMalloc((void**)&B.p_ctrace, sizeof(unsigned long long) * 8 * n, HOSTMEM) == hipSuccess) B.ctrace_cap = n;
     }
-    P.ctrace = c->d_ctrace;
+    P.ctrace = B.p_ctrace;
   }
   P.n_coarse = c->n_coarse; P.n_iv = c->n_iv; P.step = c->step;
   P.eval_range = eval_range; P.bp_resl = bp_resl; P.n_cells = n; P.mode = mode;
   return P;
 }
 
-// one launch of search_maxpos_kernel with n blocks (events recorded by the caller)
-static int launch_blocks(fsclg_ctx* c, const Params& P, int n) {
+// one launch of search_maxpos_kernel with n blocks on the batch's stream (events recorded by the caller)
+static int launch_blocks(hipStream_t stream, const Params& P, int n) {
   const int grid = n;
   const int dyn = P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
@@ -1820,18 +1936,10 @@ static int launch_blocks(fsclg_ctx* c, const Params& P, int n) {
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
       attr = true;
     }
-    hipLaunchKernelGGL(search_maxpos_kernel<true>, dim3(grid), dim3(WG), dyn, c->stream, P);
+    hipLaunchKernelGGL(search_maxpos_kernel<true>, dim3(grid), dim3(WG), dyn, stream, P);
   } else
-    hipLaunchKernelGGL(search_maxpos_kernel<false>, dim3(grid), dim3(WG), 0, c->stream, P);
+    hipLaunchKernelGGL(search_maxpos_kernel<false>, dim3(grid), dim3(WG), 0, stream, P);
   HIPCHK(hipGetLastError(), "launch search_maxpos_kernel");
-  return FSCLG_OK;
-}
-
-static int launch(fsclg_ctx* c, const Params& P, int n) {
-  HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
-  int r;
-  if ((r = launch_blocks(c, P, n))) return r;
-  HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
   return FSCLG_OK;
 }
 
@@ -1846,13 +1954,30 @@ static int ensure_buf(T** d, int* cap, int n) {
   *cap = k;
   return FSCLG_OK;
 }
+template <typename T>
+static int ensure_pinned(T** h, int* cap, int n) {
+  if (n <= *cap) return FSCLG_OK;
+  if (*h) hipHostFree(*h);
+  *h = nullptr; *cap = 0;
+  const int k = n < 1024 ? 1024 : n;
+  HIPCHK(hipHostMalloc((void**)h, sizeof(T) * k, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc");
+  *cap = k;
+  return FSCLG_OK;
+}
 }
 
-int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, int eval_range, int bp_resl,
-                        fsclg_point_t* out) {
-  if (!c || (!cells && n_cells) || (!out && n_cells) || n_cells < 0) return set_err(FSCLG_E_ARG, "cells");
-  if (!c->d_pr || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
-  if (n_cells == 0) return FSCLG_OK;
+static unsigned long long cell_key(const fsclg_cell_t& x) {
+  return ((unsigned long long)(uint32_t)x.chr << 58) ^ ((unsigned long long)(uint32_t)x.start_pos << 29) ^
+         (unsigned long long)(uint32_t)x.end_pos;
+}
+
+int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* cells, int n_cells, int eval_range,
+                        int bp_resl) {
+  if (!c || (!cells && n_cells) || n_cells < 0) return set_err(FSCLG_E_ARG, "cells");
+  if (batch < 0 || batch >= NBATCH || slot < 0 || slot >= NSLOT) return set_err(FSCLG_E_ARG, "batch/slot");
+  if (!c->d_pr0 || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
+  Batch& B = c->batch[batch];
+  if (B.pending) return set_err(FSCLG_E_STATE, "batch not waited for");
   // host-side shape checks before any launch
   if (eval_range < 0 || bp_resl < 0) return set_err(FSCLG_E_ARG, "eval_range/bp_resl");
   for (int i = 0; i < n_cells; i++) {
@@ -1862,111 +1987,134 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
   }
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
-  if ((r = ensure_windows(c, eval_range))) return r;
-  if ((r = ensure_io(c, n_cells))) return r;
+  B.n_cells = n_cells; B.nu = 0; B.nlaunch = 0; B.slot = slot; B.ivhist = nullptr; B.traced = false;
+  if (n_cells == 0) {
+    B.pending = true;
+    c->slot[slot].users++;
+    return FSCLG_OK;
+  }
+  if ((r = ensure_windows(c, slot, eval_range))) return r;
   // identical cells are evaluated once (permutation cells are G-aligned, so two points can
   // share one), and so is an endpoint shared by neighbouring cells (scan-chromosome.c:130-134
   // evaluates both ends of every cell): a first launch evaluates the distinct endpoints, the
   // cell launch reads them.  Same inputs, same device arithmetic: identical results.
-  auto key = [](const fsclg_cell_t& x) {
-    return ((unsigned long long)(uint32_t)x.chr << 58) ^ ((unsigned long long)(uint32_t)x.start_pos << 29) ^
-           (unsigned long long)(uint32_t)x.end_pos;
-  };
   auto pkey = [](int chr, int pos) { return ((unsigned long long)(uint32_t)chr << 32) | (uint32_t)pos; };
-  c->h_umap.clear();
-  c->h_ucells.clear();
-  c->h_uidx.resize(n_cells);
+  B.umap.clear();
+  B.ucells.clear();
+  B.uidx.resize(n_cells);
   for (int i = 0; i < n_cells; i++) {
-    auto ins = c->h_umap.emplace(key(cells[i]), (int)c->h_ucells.size());
-    if (ins.second) c->h_ucells.push_back(cells[i]);
-    c->h_uidx[i] = ins.first->second;
+    auto ins = B.umap.emplace(cell_key(cells[i]), (int)B.ucells.size());
+    if (ins.second) B.ucells.push_back(cells[i]);
+    B.uidx[i] = ins.first->second;
   }
-  const int nu = (int)c->h_ucells.size();
+  const int nu = (int)B.ucells.size();
   c->n_dup_cells += (unsigned long long)(n_cells - nu);
-  c->h_emap.clear();
-  c->h_epos.clear();
-  c->h_ucell_ep.resize(nu);
+  B.emap.clear();
+  B.epos.clear();
+  B.ucell_ep.resize(nu);
   for (int u = 0; u < nu; u++) {
-    const fsclg_cell_t& x = c->h_ucells[u];
+    const fsclg_cell_t& x = B.ucells[u];
     int e[2];
     for (int k = 0; k < 2; k++) {
       const int pos = k ? x.end_pos : x.start_pos;
-      auto ins = c->h_emap.emplace(pkey(x.chr, pos), (int)c->h_epos.size());
-      if (ins.second) c->h_epos.push_back(make_int2(x.chr, pos));
+      auto ins = B.emap.emplace(pkey(x.chr, pos), (int)B.epos.size());
+      if (ins.second) B.epos.push_back(make_int2(x.chr, pos));
       e[k] = ins.first->second;
     }
-    c->h_ucell_ep[u] = make_int2(e[0], e[1]);
+    B.ucell_ep[u] = make_int2(e[0], e[1]);
   }
-  const int ne = (int)c->h_epos.size();
+  const int ne = (int)B.epos.size();
   const bool use_ep = !getenv("FSCLG_NO_DEDUP") && (2 * nu - ne) * 8 >= nu;  // saves >= 1/8 of the endpoint work
   // longest first: each cell's cost in its last launch (permutation trials repeat the cells),
   // else a guess (cells nearer the middle of a chromosome walk further on both sides)
   std::vector<double> cost(nu);
   for (int u = 0; u < nu; u++) {
-    const fsclg_cell_t& x = c->h_ucells[u];
-    auto it = c->cell_cost.find(key(x));
+    const fsclg_cell_t& x = B.ucells[u];
+    auto it = c->cell_cost.find(cell_key(x));
     if (it != c->cell_cost.end()) { cost[u] = it->second; continue; }
     const int a = c->h_chr_start[x.chr], nn = c->h_chr_n[x.chr];
     const double lo = c->h_pos[a], hi = c->h_pos[a + nn - 1], span = hi > lo ? hi - lo : 1.0;
     const double m = std::min(std::max(x.start_pos - lo, 0.0), std::max(hi - x.start_pos, 0.0));
     cost[u] = 1e-3 * nn * (1.0 + 2.0 * m / span);
   }
-  c->h_order.resize(nu);
-  for (int u = 0; u < nu; u++) c->h_order[u] = u;
-  std::stable_sort(c->h_order.begin(), c->h_order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
-  c->h_cells.resize(nu);
-  c->h_cell_ep.resize(nu);
-  c->h_upos.resize(nu);
-  for (int k = 0; k < nu; k++) {
-    c->h_cells[k] = c->h_ucells[c->h_order[k]];
-    c->h_cell_ep[k] = c->h_ucell_ep[c->h_order[k]];
-    c->h_upos[c->h_order[k]] = k;
+  B.order.resize(nu);
+  for (int u = 0; u < nu; u++) B.order[u] = u;
+  std::stable_sort(B.order.begin(), B.order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+  if ((r = ensure_io(B, nu))) return r;
+  if (use_ep) {
+    if ((r = ensure_buf(&B.d_ept, &B.ept_cap, ne))) return r;
+    if ((r = ensure_pinned(&B.p_epos, &B.pep_cap, ne))) return r;
+    if ((r = ensure_pinned(&B.p_cell_ep, &B.pcep_cap, nu))) return r;
   }
-  if ((r = ensure_io(c, nu))) return r;
-  HIPCHK(hipMemcpyAsync(c->d_cells, c->h_cells.data(), sizeof(fsclg_cell_t) * nu, hipMemcpyHostToDevice, c->stream),
-         "copy cells");
-  Params P = make_params(c, nu, 0, eval_range, bp_resl);
+  B.upos.resize(nu);
+  for (int k = 0; k < nu; k++) {
+    B.p_cells[k] = B.ucells[B.order[k]];
+    if (use_ep) B.p_cell_ep[k] = B.ucell_ep[B.order[k]];
+    B.upos[B.order[k]] = k;
+  }
+  if (use_ep) memcpy(B.p_epos, B.epos.data(), sizeof(int2) * ne);
+  // the slot's rows and null sums first
+  HIPCHK(hipStreamWaitEvent(B.stream, c->slot[slot].ready, 0), "hipStreamWaitEvent");
+  Params P = make_params(c, B, slot, nu, 0, eval_range, bp_resl);
   if (c->hist_pending && P.n_civ > 0) {  // diagnostic builds (FSCLG_IVHIST): per phase key
     const int nh = (c->n_coarse + 2) * c->n_iv;
     if ((r = ensure_buf(&c->d_ivhist, &c->ivhist_n, nh))) return r;
-    HIPCHK(hipMemsetAsync(c->d_ivhist, 0, sizeof(unsigned long long) * nh, c->stream), "hipMemset ivhist");
+    HIPCHK(hipMemsetAsync(c->d_ivhist, 0, sizeof(unsigned long long) * nh, B.stream), "hipMemset ivhist");
     P.ivhist = c->d_ivhist;
-  }
-  if (use_ep) {
-    if ((r = ensure_buf(&c->d_epos, &c->epos_cap, ne))) return r;
-    if ((r = ensure_buf(&c->d_ept, &c->ept_cap, ne))) return r;
-    if ((r = ensure_buf(&c->d_cell_ep, &c->cell_ep_cap, nu))) return r;
-    HIPCHK(hipMemcpyAsync(c->d_epos, c->h_epos.data(), sizeof(int2) * ne, hipMemcpyHostToDevice, c->stream), "copy ep");
-    HIPCHK(hipMemcpyAsync(c->d_cell_ep, c->h_cell_ep.data(), sizeof(int2) * nu, hipMemcpyHostToDevice, c->stream),
-           "copy cell ep");
+    B.ivhist = c->d_ivhist;
+    c->hist_pending = false;
   }
   // the events bracket the kernel launches only (one or two of search_maxpos_kernel)
-  HIPCHK(hipEventRecord(c->ev0, c->stream), "hipEventRecord");
+  HIPCHK(hipEventRecord(B.ev0, B.stream), "hipEventRecord");
   if (use_ep) {
     Params E = P;
-    E.mode = 2; E.epos = c->d_epos; E.n_ep = ne; E.ept = c->d_ept; E.n_cells = (ne + 1) / 2; E.ctrace = nullptr;
-    if ((r = launch_blocks(c, E, E.n_cells))) return r;
-    P.ept = c->d_ept; P.cell_ep = c->d_cell_ep;
+    E.mode = 2; E.epos = B.p_epos; E.n_ep = ne; E.ept = B.d_ept; E.n_cells = (ne + 1) / 2; E.ctrace = nullptr;
+    if ((r = launch_blocks(B.stream, E, E.n_cells))) return r;
+    P.ept = B.d_ept; P.cell_ep = B.p_cell_ep;
     c->n_ep_saved += (unsigned long long)(2 * nu - ne);
   }
-  if ((r = launch_blocks(c, P, nu))) return r;
-  HIPCHK(hipEventRecord(c->ev1, c->stream), "hipEventRecord");
-  if (P.ivhist) {  // re-plan the LDS window from the measured histogram
+  if ((r = launch_blocks(B.stream, P, nu))) return r;
+  HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
+  HIPCHK(hipEventRecord(B.ev2, B.stream), "hipEventRecord");
+  B.traced = P.ctrace != nullptr;
+  B.nu = nu;
+  B.nlaunch = use_ep ? 2 : 1;
+  B.pending = true;
+  c->slot[slot].users++;
+  return FSCLG_OK;
+}
+
+int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
+  if (!c || batch < 0 || batch >= NBATCH) return set_err(FSCLG_E_ARG, "batch");
+  Batch& B = c->batch[batch];
+  if (!B.pending) return set_err(FSCLG_E_STATE, "batch not submitted");
+  if (!out && B.n_cells) return set_err(FSCLG_E_ARG, "out");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  B.pending = false;
+  c->slot[B.slot].users--;
+  if (B.n_cells == 0) return FSCLG_OK;
+  const int nu = B.nu;
+  // the batch's own completion (its stream may hold later batches): the D2H after ev1
+  HIPCHK(hipEventSynchronize(B.ev2), "hipEventSynchronize");
+  float ms = 0.f, t0 = 0.f, t1 = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, B.ev0, B.ev1), "hipEventElapsedTime");
+  HIPCHK(hipEventElapsedTime(&t0, c->ev_ref, B.ev0), "hipEventElapsedTime");
+  HIPCHK(hipEventElapsedTime(&t1, c->ev_ref, B.ev1), "hipEventElapsedTime");
+  c->kernel_ms += ms;
+  c->launches += (unsigned long long)B.nlaunch;
+  c->busy.emplace_back((double)t0, (double)t1);
+  if (B.ivhist) {  // re-plan the LDS window from the measured histogram
     const int nkey = c->n_coarse + 2;
     std::vector<unsigned long long> hk((size_t)nkey * c->n_iv), h(c->n_iv, 0);
-    HIPCHK(hipMemcpyAsync(hk.data(), P.ivhist, sizeof(unsigned long long) * hk.size(), hipMemcpyDeviceToHost, c->stream),
-           "copy ivhist");
-    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    HIPCHK(hipMemcpy(hk.data(), B.ivhist, sizeof(unsigned long long) * hk.size(), hipMemcpyDeviceToHost), "copy ivhist");
     for (int k = 0; k < nkey; k++)
       for (int j = 0; j < c->n_iv; j++) h[j] += hk[(size_t)k * c->n_iv + j];
     choose_window(c, std::vector<double>(h.begin(), h.end()));
-    c->hist_pending = false;
+    B.ivhist = nullptr;
   }
-  if (P.ctrace) {  // development aid: append [n, then n x (start, end, cu, terms, 4 phase times)] to the file
+  if (B.traced) {  // development aid: append [n, then n x (start, end, cu, terms, 4 phase times)] to the file
     std::vector<unsigned long long> h((size_t)8 * nu);
-    HIPCHK(hipMemcpyAsync(h.data(), P.ctrace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream),
-           "copy trace");
-    HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    memcpy(h.data(), B.p_ctrace, sizeof(unsigned long long) * h.size());
     if (FILE* f = fopen(getenv("FSCLG_CELL_TRACE"), "ab")) {
       const unsigned long long nn = (unsigned long long)nu;
       fwrite(&nn, sizeof nn, 1, f);
@@ -1974,25 +2122,29 @@ int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, in
       fclose(f);
     }
   }
-  c->h_out.resize(nu);
-  HIPCHK(hipMemcpyAsync(c->h_out.data(), c->d_out, sizeof(fsclg_point_t) * nu, hipMemcpyDeviceToHost, c->stream),
-         "copy out");
-  HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
-  float ms = 0.f;
-  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
-  c->kernel_ms += ms;
-  c->launches += use_ep ? 2 : 1;
-  for (int k = 0; k < nu; k++) c->cell_cost[key(c->h_cells[k])] = c->h_out[k].cost;
-  for (int i = 0; i < n_cells; i++) out[i] = c->h_out[c->h_upos[c->h_uidx[i]]];
-  for (int i = 0; i < n_cells; i++)
+  for (int k = 0; k < nu; k++) c->cell_cost[cell_key(B.p_cells[k])] = B.p_out[k].cost;
+  for (int i = 0; i < B.n_cells; i++) out[i] = B.p_out[B.upos[B.uidx[i]]];
+  for (int i = 0; i < B.n_cells; i++)
     if (out[i].flags) return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL, "device flag");
   return FSCLG_OK;
 }
 
+int fsclg_search_maxpos(fsclg_ctx* c, const fsclg_cell_t* cells, int n_cells, int eval_range, int bp_resl,
+                        fsclg_point_t* out) {
+  if (!c || (!cells && n_cells) || (!out && n_cells) || n_cells < 0) return set_err(FSCLG_E_ARG, "cells");
+  if (!c->d_pr0 || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
+  if (n_cells == 0) return FSCLG_OK;
+  int r = fsclg_search_submit(c, 0, 0, cells, n_cells, eval_range, bp_resl);
+  if (r) return r;
+  return fsclg_search_wait(c, 0, out);
+}
+
 int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
   if (!c || (!pts && n_pts) || n_pts < 0) return set_err(FSCLG_E_ARG, "points");
-  if (!c->d_pr || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
+  if (!c->d_pr0 || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
   if (n_pts == 0) return FSCLG_OK;
+  Batch& B = c->batch[0];
+  if (B.pending) return set_err(FSCLG_E_STATE, "batch 0 not waited for");
   for (int i = 0; i < n_pts; i++) {
     const fsclg_point_t& p = pts[i];
     if (p.window_start < 0 || p.window_end >= c->n_snps || p.window_start > p.window_end ||
@@ -2002,16 +2154,22 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
   }
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
-  if ((r = ensure_io(c, n_pts))) return r;
-  HIPCHK(hipMemcpyAsync(c->d_out, pts, sizeof(fsclg_point_t) * n_pts, hipMemcpyHostToDevice, c->stream), "copy pts");
-  Params P = make_params(c, n_pts, 1, 0, 0);
-  if ((r = launch(c, P, n_pts))) return r;
-  HIPCHK(hipMemcpyAsync(pts, c->d_out, sizeof(fsclg_point_t) * n_pts, hipMemcpyDeviceToHost, c->stream), "copy out");
-  HIPCHK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
-  float ms = 0.f;
-  HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1), "hipEventElapsedTime");
+  if ((r = ensure_io(B, n_pts))) return r;
+  HIPCHK(hipStreamWaitEvent(B.stream, c->slot[0].ready, 0), "hipStreamWaitEvent");
+  memcpy(B.p_out, pts, sizeof(fsclg_point_t) * n_pts);  // read and written in place by the kernel
+  Params P = make_params(c, B, 0, n_pts, 1, 0, 0);
+  HIPCHK(hipEventRecord(B.ev0, B.stream), "hipEventRecord");
+  if ((r = launch_blocks(B.stream, P, n_pts))) return r;
+  HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
+  HIPCHK(hipEventSynchronize(B.ev1), "hipEventSynchronize");
+  memcpy(pts, B.p_out, sizeof(fsclg_point_t) * n_pts);
+  float ms = 0.f, t0 = 0.f, t1 = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, B.ev0, B.ev1), "hipEventElapsedTime");
+  HIPCHK(hipEventElapsedTime(&t0, c->ev_ref, B.ev0), "hipEventElapsedTime");
+  HIPCHK(hipEventElapsedTime(&t1, c->ev_ref, B.ev1), "hipEventElapsedTime");
   c->kernel_ms += ms;
   c->launches++;
+  c->busy.emplace_back((double)t0, (double)t1);
   return FSCLG_OK;
 }
 
@@ -2032,6 +2190,17 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
   st->n_unsafe = h[4]; st->n_slow = h[5]; st->n_ties = h[6]; st->n_cells = h[7];
   st->kernel_ms = c->kernel_ms; st->n_launches = c->launches; st->window_ms = c->window_ms;
   st->n_dup_cells = c->n_dup_cells; st->n_ep_saved = c->n_ep_saved;
+  {  // union of the batches' kernel intervals
+    std::vector<std::pair<double, double>> iv(c->busy);
+    std::sort(iv.begin(), iv.end());
+    double busy = 0.0, a = 0.0, b = -1.0;
+    for (const auto& x : iv) {
+      if (x.first > b) { if (b > a) busy += b - a; a = x.first; b = x.second; }
+      else b = std::max(b, x.second);
+    }
+    if (b > a) busy += b - a;
+    st->busy_ms = busy;
+  }
   if (c->plan_dirty) plan_cache(c);
   st->cache_iv0 = c->c_ivc0; st->cache_n_iv = c->c_civ; st->cache_n_rows = c->c_crow; st->cache_cover = c->c_cover;
   return FSCLG_OK;
@@ -2042,6 +2211,7 @@ int fsclg_reset_stats(fsclg_ctx* c) {
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
   c->kernel_ms = 0.0; c->launches = 0; c->window_ms = 0.0; c->n_dup_cells = 0; c->n_ep_saved = 0;
+  c->busy.clear();
   return FSCLG_OK;
 }
 

@@ -488,6 +488,243 @@ static void on_sigint(int sig) { /* scan-chromosome.c:557-569 */
 
 static void output_clr_null_distribution(const char *fname, scan_t *s);
 
+/* ------------------------------------------------ pipelined permutation trials
+   scan-chromosome.c:582-652 with --n-threads=1 pruning semantics, K = FSCLG_N_SLOTS trials
+   in flight.  What orders the trials is the rand() stream: trial t+1's permutation depends on
+   the draws of trial t, and a point draws only on a hit that takes its permute_p to >= 20
+   (scan-chromosome.c:488-498); only those points can be pruned.  Each point keeps a queue of
+   its results by trial, applied strictly in trial order; u = permute_p + queued results is an
+   upper bound of permute_p before the next trial.
+     * points with u >= 20 - K ("near-critical") form the trial's blocking batch, on the
+       high-priority stream; the next permutation is built once it has been applied;
+     * the rest form a bulk batch on a normal stream, waited only when its row slot comes
+       round again (K trials later).
+   A point with u <= 19 cannot draw in any queued trial (its permute_p stays <= 19 through
+   them), so results may be applied late without changing a draw.  A point enters the
+   near-critical class at u = 20 - K and can draw no earlier than K - 1 trials later, by when
+   its bulk results have been waited for: each trial's draws happen in point order after its
+   own permutation, as in the lockstep loop (a violation is caught and the pending batches
+   are drained first; never seen, counted in stats).  Results are identical to the lockstep
+   order (FSCL_AMD_LOCKSTEP=1). */
+#define PQ (FSCLG_N_SLOTS + 2)
+typedef struct {
+  int trial;
+  int have;
+  double clr, lalpha;
+  int start_pos;
+} pres_t;
+typedef struct {
+  pres_t e[PQ];
+  int head, n;
+} pqueue_t;
+
+typedef struct {
+  int batch;              /* device batch */
+  int trial;
+  int n, cap;
+  int *pt;                /* scan point of each cell, ascending */
+  fsclg_cell_t *cells;
+  fsclg_point_t *out;
+  int submitted;
+} trial_batch_t;
+
+static void tb_reserve(trial_batch_t *b, int n) {
+  if (n <= b->cap) return;
+  b->cap = n;
+  b->pt = fh_realloc(b->pt, sizeof(int) * n, "batch");
+  b->cells = fh_realloc(b->cells, sizeof(fsclg_cell_t) * n, "batch");
+  b->out = fh_realloc(b->out, sizeof(fsclg_point_t) * n, "batch");
+}
+
+static void tb_free(trial_batch_t *b) { free(b->pt); free(b->cells); free(b->out); memset(b, 0, sizeof *b); }
+
+/* this rank's contiguous share of a batch (a cell's work scales with its window) */
+static void tb_share(const trial_batch_t *b, int eval_range, int *lo, int *hi) {
+  double *cost;
+  int i;
+  *lo = 0; *hi = b->n;
+  if (D.world <= 1) return;
+  cost = fh_malloc(sizeof(double) * (b->n ? b->n : 1), "cost");
+  for (i = 0; i < b->n; i++)
+    cost[i] = (double)(D.chr_n[b->cells[i].chr] < 2 * eval_range + 1 ? D.chr_n[b->cells[i].chr] : 2 * eval_range + 1);
+  rank_share(cost, b->n, lo, hi);
+  free(cost);
+}
+
+static void tb_submit(trial_batch_t *b, int slot, int eval_range, int bp_resl) {
+  int lo, hi;
+  tb_share(b, eval_range, &lo, &hi);
+  if (D.world > 1) memset(b->out, 0, sizeof(fsclg_point_t) * b->n);
+  dev_check(fsclg_search_submit(D.ctx, b->batch, slot, b->cells + lo, hi - lo, eval_range, bp_resl), "search submit");
+  b->submitted = 1;
+  D.st.gp_evals += (unsigned long long)(hi - lo);
+}
+
+/* wait for a batch and file each result in its point's queue */
+static void tb_wait(trial_batch_t *b, pqueue_t *pq, int eval_range) {
+  int lo, hi, k;
+  double tw = fh_now();
+  if (!b->submitted) return;
+  tb_share(b, eval_range, &lo, &hi);
+  dev_check(fsclg_search_wait(D.ctx, b->batch, b->out + lo), "search wait");
+  b->submitted = 0;
+  D.st.wait_s += fh_now() - tw;
+  if (D.world > 1) exchange((long long *)b->out, (int)(b->n * (sizeof(fsclg_point_t) / sizeof(long long))));
+  for (k = 0; k < b->n; k++) {
+    pqueue_t *q = pq + b->pt[k];
+    int j;
+    for (j = 0; j < q->n; j++) {
+      pres_t *e = q->e + (q->head + j) % PQ;
+      if (e->trial == b->trial) {
+        e->have = 1; e->clr = b->out[k].clr; e->lalpha = b->out[k].lalpha; e->start_pos = b->cells[k].start_pos;
+        break;
+      }
+    }
+    if (j == q->n) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline lost a result");
+  }
+}
+
+/* apply point i's queued results in trial order, up to trial `upto`; only trial `draw`
+   may draw rand() (scan-chromosome.c:488-502) */
+static void pq_flush(scan_t *s, pqueue_t *pq, int i, int upto, int draw, fh_rand_t *g, int save) {
+  pqueue_t *q = pq + i;
+  scan_pt_t *p = s->scan_pts + i;
+  while (q->n > 0) {
+    pres_t *e = q->e + q->head;
+    if (!e->have || e->trial > upto) break;
+    if (e->clr >= p->clr) {
+      p->permute_p++;
+      if (p->permute_p >= 20) {
+        if (e->trial != draw) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline: out-of-order rand draw");
+        if (p->permute_p / (double)p->permute_n >= fh_rand(g) / (2147483647 + 1.0))
+          p->permute_finished = 1; /* Q7: ratio uses the pre-increment count */
+      }
+    }
+    if (p->permute_n < save) p->permute_clr[p->permute_n] = (float)e->clr;
+    p->permute_n++;
+    if (e->clr < 0 || e->clr > 1000000 || isnan(e->clr))
+      fprintf(stderr, "%d\t%d\t%g\t%1.3e\n", p->chr, e->start_pos, e->clr, exp(e->lalpha));
+    q->head = (q->head + 1) % PQ;
+    q->n--;
+  }
+}
+
+static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eval_range, int bp_resl,
+                              int large_grid_sp, double scan_width_mb, fh_rand_t *g, int save) {
+  enum { K = FSCLG_N_SLOTS };
+  int *act, n_act = s->n_scan_pts, i, k, trial = -1, done = -1;
+  pqueue_t *pq;
+  double *nul[K];
+  trial_batch_t A, Bt[K];
+  memset(&A, 0, sizeof A);
+  memset(Bt, 0, sizeof Bt);
+  A.batch = 0; /* high-priority stream */
+  for (k = 0; k < K; k++) { Bt[k].batch = 2 + k; nul[k] = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums"); }
+  act = fh_malloc(sizeof(int) * (n_act ? n_act : 1), "active points");
+  pq = fh_calloc(n_act ? n_act : 1, sizeof(pqueue_t), "result queues");
+  tb_reserve(&A, n_act ? n_act : 1);
+  for (k = 0; k < K; k++) tb_reserve(&Bt[k], n_act ? n_act : 1);
+  for (i = 0; i < n_act; i++) act[i] = i;
+  for (;;) {
+    const int slot = (trial + 1) % K;
+    trial_batch_t *B = &Bt[slot];
+    double tp = fh_now();
+    uint32_t *prow;
+    /* the slot's previous trial: its bulk results (no draws among them) */
+    if (B->submitted) {
+      tb_wait(B, pq, eval_range);
+      for (k = 0; k < B->n; k++) pq_flush(s, pq, B->pt[k], done, -1, g, save);
+    }
+    D.st.search_s += fh_now() - tp;
+    tp = fh_now();
+    prow = fsclg_slot_row_buffer(D.ctx, slot);
+    if (!prow) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
+    block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g);
+    D.st.host_perm_s += fh_now() - tp;
+    trial++;
+    for (i = k = 0; i < n_act; i++)
+      if (!s->scan_pts[act[i]].permute_finished) act[k++] = act[i];
+    n_act = k;
+    cr_logmsg(MSG_STATUS, "Scanning snp block permutations... %7d (%d scan pts remaining)        ", trial, n_act);
+    if (n_act == 0 || trial > n_perm) break;
+    tp = fh_now();
+    chr_null_sums(prow, nul[slot]);
+    D.st.host_null_s += fh_now() - tp;
+    tp = fh_now();
+    dev_check(fsclg_slot_set_rows(D.ctx, slot, prow, nul[slot]), "set rows");
+    D.st.host_upload_s += fh_now() - tp;
+    tp = fh_now();
+    A.n = B->n = 0;
+    A.trial = B->trial = trial;
+    for (i = 0; i < n_act; i++) {
+      const int a = act[i];
+      const scan_pt_t *q = s->scan_pts + a;
+      trial_batch_t *b = q->permute_p + pq[a].n >= 20 - K ? &A : B;
+      fsclg_cell_t *cl = b->cells + b->n;
+      pres_t *e = pq[a].e + (pq[a].head + pq[a].n) % PQ;
+      if (pq[a].n == PQ) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline queue overflow");
+      cl->chr = q->chr;
+      cl->start_pos = q->sweep_pos - (q->sweep_pos % large_grid_sp); /* Q5: G-aligned, unclipped */
+      cl->end_pos = cl->start_pos + large_grid_sp;
+      cl->pad = 0;
+      b->pt[b->n++] = a;
+      e->trial = trial; e->have = 0;
+      pq[a].n++;
+    }
+    D.st.n_crit += (unsigned long long)A.n;
+    if (A.n) tb_submit(&A, slot, eval_range, bp_resl);
+    if (B->n) tb_submit(B, slot, eval_range, bp_resl);
+    if (A.submitted) {
+      int drain = 0;
+      tb_wait(&A, pq, eval_range);
+      /* a point that may draw in this trial needs every earlier result applied first */
+      for (k = 0; k < A.n && !drain; k++) {
+        const int a = A.pt[k];
+        if (s->scan_pts[a].permute_p + pq[a].n >= 20)
+          for (i = 0; i < pq[a].n; i++)
+            if (!pq[a].e[(pq[a].head + i) % PQ].have) drain = 1;
+      }
+      if (drain) { /* never expected: wait the bulk batches in trial order */
+        D.st.n_drain++;
+        for (;;) {
+          trial_batch_t *old = NULL;
+          for (k = 0; k < K; k++)
+            if (Bt[k].submitted && Bt[k].trial < trial && (!old || Bt[k].trial < old->trial)) old = &Bt[k];
+          if (!old) break;
+          tb_wait(old, pq, eval_range);
+          for (k = 0; k < old->n; k++) pq_flush(s, pq, old->pt[k], trial - 1, -1, g, save);
+        }
+      }
+      for (k = 0; k < A.n; k++) pq_flush(s, pq, A.pt[k], trial, trial, g, save); /* ascending point order */
+    }
+    done = trial;
+    D.st.search_s += fh_now() - tp;
+    D.st.trials++;
+    if (g_sigint && D.rank == 0) {
+      g_sigint = 0;
+      scan_output(output_fname, s, 0, n_permute, prepend_label);
+      if (output_fname) output_clr_null_distribution(output_fname, s);
+      gettimeofday(&g_last_dump, NULL);
+    }
+  }
+  /* the bulk batches still in flight, oldest first */
+  for (;;) {
+    trial_batch_t *old = NULL;
+    double tp = fh_now();
+    for (k = 0; k < K; k++)
+      if (Bt[k].submitted && (!old || Bt[k].trial < old->trial)) old = &Bt[k];
+    if (!old) break;
+    tb_wait(old, pq, eval_range);
+    for (k = 0; k < old->n; k++) pq_flush(s, pq, old->pt[k], done, -1, g, save);
+    D.st.search_s += fh_now() - tp;
+  }
+  for (i = 0; i < s->n_scan_pts; i++)
+    if (pq[i].n) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline: unapplied results");
+  tb_free(&A);
+  for (k = 0; k < K; k++) { tb_free(&Bt[k]); free(nul[k]); }
+  free(act); free(pq);
+}
+
 /* scan-chromosome.c:582-652 (with --n-threads=1 pruning semantics) */
 void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, double alpha_factor, int n_threads,
                   int eval_range, int bp_resl, int large_grid_sp, double scan_width_mb) {
@@ -508,17 +745,21 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   sigaction(SIGINT, &sa, NULL);
   fh_srand(&g, PERM_SEED);
   (void)fh_rand(&g); /* scan-chromosome.c:440: the single thread's usleep() draw */
-  /* the permutation is written straight into the device context's pinned staging */
+  for (i = 0; i < s->n_scan_pts; i++)
+    if (!s->scan_pts[i].permute_clr) s->scan_pts[i].permute_clr = fh_malloc(sizeof(float) * (save > 0 ? save : 1), "permute_clr");
+  if (!getenv("FSCL_AMD_LOCKSTEP") && s->n_scan_pts <= (1 << 16)) {
+    permute_pipelined(s, n_perm, permute_nbp, eval_range, bp_resl, large_grid_sp, scan_width_mb, &g, save);
+    goto done;
+  }
+  /* lockstep: permute -> rows to the device -> every active cell -> prune.  The permutation
+     is written straight into the device context's pinned staging */
   prow = fsclg_row_buffer(D.ctx);
   if (!prow) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
   act = fh_malloc(sizeof(int) * (n_act ? n_act : 1), "active points");
   cells = fh_malloc(sizeof(fsclg_cell_t) * (n_act ? n_act : 1), "cells");
   out = fh_malloc(sizeof(fsclg_point_t) * (n_act ? n_act : 1), "points");
   nul = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
-  for (i = 0; i < s->n_scan_pts; i++) {
-    act[i] = i;
-    if (!s->scan_pts[i].permute_clr) s->scan_pts[i].permute_clr = fh_malloc(sizeof(float) * (save > 0 ? save : 1), "permute_clr");
-  }
+  for (i = 0; i < s->n_scan_pts; i++) act[i] = i;
   for (;;) {
     double tp = fh_now();
     block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, &g);
@@ -569,10 +810,11 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
       gettimeofday(&g_last_dump, NULL);
     }
   }
+  free(act); free(cells); free(out); free(nul);
+done:
   cr_logmsg(MSG_STATUS, "Scanning snp block permutations... finished.\n");
   signal(SIGINT, SIG_DFL);
   dev_check(fsclg_set_rows(D.ctx, NULL), "set rows");
-  free(act); free(cells); free(out); free(nul);
   D.st.permute_s += fh_now() - t0;
 }
 
@@ -696,6 +938,7 @@ void fscl_amd_get_stats(fscl_amd_stats_t *st) {
       st->cache_iv0 = g.cache_iv0; st->cache_n_iv = g.cache_n_iv; st->cache_n_rows = g.cache_n_rows;
       st->cache_cover = g.cache_cover; st->window_ms = g.window_ms;
       st->n_dup_cells = g.n_dup_cells; st->n_ep_saved = g.n_ep_saved;
+      st->busy_ms = g.busy_ms;
     }
   }
 }

@@ -174,6 +174,10 @@ typedef struct {
   double search_s;        /*   cell evaluation (launch, kernel, results, rank exchange) */
   double prune_s;         /*   pruning and bookkeeping */
   unsigned long long n_dup_cells, n_ep_saved;  /* fsclg_stats_t: work shared between cells */
+  double busy_ms;         /* fsclg_stats_t: union of the search kernels' intervals (overlap counted once) */
+  double wait_s;          /* scan_permute: host time blocked on trial results */
+  unsigned long long n_crit;  /* scan_permute: cells in the trials' blocking (near-critical) batches */
+  unsigned long long n_drain; /* scan_permute: trials that had to wait for every bulk batch in flight */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

@@ -15,6 +15,10 @@
  *                           sm-search.c:269-300 (fscl.h:105)
  *   fsclg_set_rows       -> the permuted snp array of one trial,
  *                           scan-chromosome.c:443 (snp_block_permute output)
+ *   fsclg_slot_set_rows  -> the same for one of FSCLG_N_SLOTS trials in flight
+ *   fsclg_search_submit/ -> the per-trial search_maxpos calls of
+ *   fsclg_search_wait       scan_permute_thread (scan-chromosome.c:478-487),
+ *                           split so that consecutive trials overlap on the GPU
  *   fsclg_upload_tables  -> sm_ptable_t spline tables (fscl.h:64-76) and
  *                           log_table (sm-search.c:14-26)
  *   fsclg_upload_snps    -> snp_t positions + chr_limits_t (fscl.h:7-33)
@@ -68,7 +72,16 @@ typedef struct {
   double window_ms;                /* summed duration of the window null-sum kernels (HIP events) */
   unsigned long long n_dup_cells;  /* cells answered by an identical cell of the same launch */
   unsigned long long n_ep_saved;   /* endpoint evaluations saved by sharing between neighbouring cells */
+  double busy_ms;                  /* union of the search batches' kernel intervals (overlapping batches
+                                      counted once): the GPU time the search kernels occupied */
 } fsclg_stats_t;
+
+/* trials in flight: row slots (one permuted row array + null sums each) and launch batches
+   (cells and outputs each).  Batches 0 and 1 run on one high-priority stream, batches
+   2 .. FSCLG_N_BATCHES-1 on two normal-priority streams (even / odd batch): with the upload
+   stream, four streams, one per hardware queue (GPU_MAX_HW_QUEUES = 4) */
+#define FSCLG_N_SLOTS 4
+#define FSCLG_N_BATCHES 6
 
 int fsclg_open(int device, fsclg_ctx **out);
 int fsclg_close(fsclg_ctx *c);
@@ -93,6 +106,21 @@ int fsclg_upload_snps(fsclg_ctx *c, const int32_t *pos, const uint32_t *row, int
    fsclg_set_rows (the buffer may be rewritten once fsclg_set_rows's search has returned) */
 uint32_t *fsclg_row_buffer(fsclg_ctx *c);
 int fsclg_set_rows(fsclg_ctx *c, const uint32_t *row);
+
+/* asynchronous trials.  A row slot holds one trial's rows on the device; a batch is one
+   search_maxpos launch over the rows of one slot.  fsclg_slot_row_buffer returns the slot's
+   pinned staging buffer (NULL while a batch submitted on the slot is not waited for);
+   fsclg_slot_set_rows uploads it (or row, or the uploaded rows when row is NULL) and, when
+   chr_null is not NULL, the slot's whole-chromosome null sums; both are asynchronous and
+   fail with FSCLG_E_STATE while the slot is in use.  fsclg_search_submit queues a batch
+   (cells are copied; the batch must be idle) and returns at once; fsclg_search_wait blocks
+   until its points are in out[n_cells] (input order).  Slot 0 and batch 0 are also what the
+   synchronous calls (fsclg_set_rows, fsclg_search_maxpos) use. */
+uint32_t *fsclg_slot_row_buffer(fsclg_ctx *c, int slot);
+int fsclg_slot_set_rows(fsclg_ctx *c, int slot, const uint32_t *row, const double *chr_null);
+int fsclg_search_submit(fsclg_ctx *c, int batch, int slot, const fsclg_cell_t *cells, int n_cells, int eval_range,
+                        int bp_resl);
+int fsclg_search_wait(fsclg_ctx *c, int batch, fsclg_point_t *out);
 
 /* sequential window null sums (init_scan_result's sum from 0.0) for each chromosome's
    whole-chromosome window, for the rows currently set */

@@ -206,6 +206,29 @@ def test_two_ranks_on_one_gpu_match_one_rank(built, tmp):
     assert not (tmp / "o1.txt").exists()  # one writer
 
 
+def test_pipelined_trials_match_lockstep_and_oracle(built, tmp, monkeypatch):
+    """Two trials in flight (scan_permute's default): the rand-stream critical points
+    (permute_p >= 19) run ahead of the rest of their trial, the next trial's permutation is
+    built and launched before the rest has finished.  Enough trials that points cross the
+    critical threshold, draw rand() and are pruned: identical to the lockstep order
+    (FSCL_AMD_LOCKSTEP=1) and to the oracle, bit for bit."""
+    snp = tmp / "pipe.snp"
+    synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=8_000_000, snps_per_chr=8000, n=30, seed=81,
+                                                  sweeps_per_chr=2))
+    opts = ["--coarse-grid-spacing=40000", "--n-permute=70"]
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    fscl_amd.reset_stats()
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
+    st = fscl_amd.get_stats()
+    pts = fscl_amd.points(scan)
+    assert st["n_crit"] > 0 and (pts["permute_n"] < 71).any()  # critical batches ran, points were pruned
+    assert_rows_equal(points_rows(pts), read_dump(tmp / "o.dump"), "pipelined")
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+    monkeypatch.setenv("FSCL_AMD_LOCKSTEP", "1")
+    scan = fscl_amd.run(snp, tmp / "l.txt", **_kw(opts))
+    assert (tmp / "l.txt").read_text() == (tmp / "o.txt").read_text()
+
+
 def test_c2_scale_scan_and_short_permutation(built, tmp):
     """BASELINE config 2 (100k SNPs, n=100, 200 Mb) at full size: the whole
     initial scan and 3 permutation trials, bit-exact against the oracle."""
