@@ -489,8 +489,8 @@ static void on_sigint(int sig) { /* scan-chromosome.c:557-569 */
 static void output_clr_null_distribution(const char *fname, scan_t *s);
 
 /* ------------------------------------------------ pipelined permutation trials
-   scan-chromosome.c:582-652 with --n-threads=1 pruning semantics, K = FSCLG_N_SLOTS trials
-   in flight.  What orders the trials is the rand() stream: trial t+1's permutation depends on
+   scan-chromosome.c:582-652 with --n-threads=1 pruning semantics, K trials in flight
+   (FSCL_AMD_DEPTH, default 4, at most FSCLG_N_SLOTS).  What orders the trials is the rand() stream: trial t+1's permutation depends on
    the draws of trial t, and a point draws only on a hit that takes its permute_p to >= 20
    (scan-chromosome.c:488-498); only those points can be pruned.  Each point keeps a queue of
    its results by trial, applied strictly in trial order; u = permute_p + queued results is an
@@ -611,11 +611,12 @@ static void pq_flush(scan_t *s, pqueue_t *pq, int i, int upto, int draw, fh_rand
 
 static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eval_range, int bp_resl,
                               int large_grid_sp, double scan_width_mb, fh_rand_t *g, int save) {
-  enum { K = FSCLG_N_SLOTS };
+  const char *env = getenv("FSCL_AMD_DEPTH");
+  const int K = env ? (atoi(env) < 2 ? 2 : (atoi(env) > FSCLG_N_SLOTS ? FSCLG_N_SLOTS : atoi(env))) : 4;
   int *act, n_act = s->n_scan_pts, i, k, trial = -1, done = -1;
   pqueue_t *pq;
-  double *nul[K];
-  trial_batch_t A, Bt[K];
+  double *nul[FSCLG_N_SLOTS];
+  trial_batch_t A, Bt[FSCLG_N_SLOTS];
   memset(&A, 0, sizeof A);
   memset(Bt, 0, sizeof Bt);
   A.batch = 0; /* high-priority stream */

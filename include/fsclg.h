@@ -80,8 +80,8 @@ typedef struct {
    (cells and outputs each).  Batches 0 and 1 run on one high-priority stream, batches
    2 .. FSCLG_N_BATCHES-1 on two normal-priority streams (even / odd batch): with the upload
    stream, four streams, one per hardware queue (GPU_MAX_HW_QUEUES = 4) */
-#define FSCLG_N_SLOTS 4
-#define FSCLG_N_BATCHES 6
+#define FSCLG_N_SLOTS 8
+#define FSCLG_N_BATCHES 10
 
 int fsclg_open(int device, fsclg_ctx **out);
 int fsclg_close(fsclg_ctx *c);

@@ -19,6 +19,25 @@ for row in csv.DictReader(open(src / "trace" / "run_kernel_stats.csv")):
         out["trace"] = {"calls": int(row["Calls"]), "avg_ms": float(row["AverageNs"]) / 1e6,
                         "min_ms": float(row["MinNs"]) / 1e6, "max_ms": float(row["MaxNs"]) / 1e6,
                         "share_pct": float(row["Percentage"])}
+# launches of different batch streams overlap: the GPU time they occupy is the union of
+# their intervals (bench.py divides by the same union, measured with HIP events)
+kt = src / "trace" / "run_kernel_trace.csv"
+if kt.exists():
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(kt))
+                if "search_maxpos" in r["Kernel_Name"])
+    busy, a, b = 0, None, None
+    for s0, e0 in iv:
+        if b is None or s0 > b:
+            if b is not None:
+                busy += b - a
+            a, b = s0, e0
+        else:
+            b = max(b, e0)
+    if b is not None:
+        busy += b - a
+    out["trace_union"] = {"calls": len(iv), "busy_ms": busy / 1e6,
+                          "busy_ms_per_launch": busy / 1e6 / max(1, len(iv)),
+                          "sum_ms": sum(e0 - s0 for s0, e0 in iv) / 1e6}
 pmc = {}
 for grp in ("fetch", "write", "sq"):
     f = src / grp / "run_counter_collection.csv"
@@ -42,6 +61,8 @@ for name in ("bench_trace.json", "bench_fetch.json"):
     if p.exists() and p.read_text().strip():
         b = json.loads(p.read_text().strip().splitlines()[-1])
         out.setdefault("bench", {})[name] = {"avg_launch_ms_hip_events": b["roofline"]["avg_launch_ms"],
+                                             "busy_ms_per_launch_hip_events":
+                                                 b["roofline"].get("busy_ms", 0.0) / max(1, b["roofline"]["launches"]),
                                              "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"],
                                              "value": b["value"], "ms_per_step": b["ms_per_step"]}
 json.dump(out, open(f"{dst}_summary.json", "w"), indent=1)
