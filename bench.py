@@ -201,7 +201,7 @@ def main() -> int:
         sys.path.insert(0, str(ROOT / "oracle"))
         from oracle import OracleScan  # noqa: E402  (test infrastructure: the CPU baseline leg only)
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        orc = OracleScan(snp, threads=threads)
+        orc = OracleScan(snp, threads=threads, asc_depth=cfg.get("asc_depth", 0), asc_min_freq=cfg.get("asc_min_freq", 1))
         t0 = time.perf_counter()
         orc.scan()
         cpu_s = time.perf_counter() - t0

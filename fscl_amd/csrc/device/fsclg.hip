@@ -150,6 +150,7 @@ struct Smem {
   Walk w[MAXWALK];
   unsigned long long P[MAXWALK];
   unsigned long long Q[MAXWALK];
+  double Pd[MAXWALK], Qd[MAXWALK];  // fp64 sums of the lanes whose accumulators passed 2^51 (approximate)
   unsigned int segbits[MAXWALK][SEGWORDS];
   int wflag[MAXWALK];
   int exact[MAXWALK];
@@ -431,7 +432,13 @@ __device__ __forceinline__ void walk_bounds_par(Smem& S, const Params& P, int ti
   }
 }
 
-// exact sequential sum of one walk by one wave (slow path, settles an argmax)
+// exact sequential sum of one walk by one wave (slow path, settles an argmax), 64 terms at
+// a time.  A chunk whose partial sums provably stay inside the binade of the running value
+// acc (u = its ulp) and holds no tie adds exactly acc + u * sum(rint(t/u)) (SURVEY Appendix
+// B, per chunk): one wave reduction.  Otherwise (a binade edge within reach, a tie, acc >= 0)
+// the chunk is added term by term as the reference does.  Walks that leave the binade of the
+// window null sum (ascertainment-corrected tables: sums far below null) cross a few binades,
+// so almost every chunk takes the reduction.
 template <bool LDS>
 __device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, const Params& P, int lane) {
   double acc = pt.N;
@@ -439,8 +446,28 @@ __device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, 
     const int k = kb + lane;
     double t = 0.0;
     if (k < W.len) t = term_dev<LDS>(walk_index(k, pt.nearest, W.nl), pt.sweep, W.la, S, P);
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(acc);
+    const int be = (int)((bits >> 52) & 0x7FF);
+    if (acc < 0.0 && be > 52 && be < 0x7FF - 52) {
+      const double inv = __longlong_as_double((long long)(2098 - be) << 52);   // 2^(52 - e), e = be - 1023
+      const double u = __longlong_as_double((long long)(be - 52) << 52);       // 2^(e - 52)
+      const double q = t * inv, R = rint(q);
+      if (!__any(fabs(q - R) == 0.5) && !__any(!(fabs(R) < 4503599627370496.0))) {  // no tie, |R| < 2^52
+        double sp = R > 0.0 ? R : 0.0, sn = R < 0.0 ? R : 0.0;  // |sums| < 2^58: exact only below 2^53,
+#pragma unroll                                                  // checked by the bounds below
+        for (int o = 32; o > 0; o >>= 1) { sp += __shfl_xor(sp, o, 64); sn += __shfl_xor(sn, o, 64); }
+        const double A0 = acc * inv;  // an integer in (-2^53, -2^52]
+        // every partial lies in [A0 + sn, A0 + sp]; inside (-2^53, -2^52] it stays in the binade
+        if (sp < 9007199254740992.0 && sn > -9007199254740992.0 && A0 + sn > -9007199254740992.0 &&
+            A0 + sp <= -4503599627370496.0) {
+          acc = (A0 + sp + sn) * u;
+          continue;
+        }
+      }
+    }
     const int lim = W.len - kb < 64 ? W.len - kb : 64;
     for (int l = 0; l < lim; l++) acc = acc + __shfl(t, l, 64);
+    if (acc != acc) break;  // NaN stays NaN through every later add (NaN spline rows, Q15)
   }
   return acc;
 }
@@ -781,7 +808,16 @@ __device__ __forceinline__ void flush_walk(Smem& S, int w, double acc, double ac
   if (lane == 0) {
     atomicAdd(&S.P[w], (unsigned long long)isum);
     atomicAdd(&S.Q[w], (unsigned long long)imag);
-    if (anybig) atomicOr(&S.wflag[w], 1);
+  }
+  if (anybig) {  // rare (terms near log(DBL_MIN) of ascertainment-corrected tables): approximate sums
+    double da = big ? acc : 0.0, dm = big ? accm : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { da += __shfl_xor(da, o, 64); dm += __shfl_xor(dm, o, 64); }
+    if (lane == 0) {
+      atomicAdd(&S.Pd[w], da);
+      atomicAdd(&S.Qd[w], dm);
+      atomicOr(&S.wflag[w], 1);
+    }
   }
 }
 
@@ -799,7 +835,7 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
   const int nt = S.n_ties < MAXTIES ? S.n_ties : MAXTIES;
   for (int j = 0; j < nt; j++) T += (((S.ties[j] >> 20) & 31) == w);
   const bool big = S.wflag[w] != 0 || pt.inv_u == 0.0;
-  const long long S0 = big ? 0 : (long long)(pt.N * pt.inv_u);
+  const long long S0 = pt.inv_u == 0.0 ? 0 : (long long)(pt.N * pt.inv_u);
   const long long LO = -(1ll << 53), HI = -((1ll << 52) + 1);
   const bool safe = !big && !overflow && S0 < 0 && (S0 + Qn - T >= LO) && (S0 + Pp + T <= HI);
   if (safe) {
@@ -835,9 +871,19 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
     S.val[w] = (double)(S0 + Ssum + adjs) * pt.u;
   } else {
     S.exact[w] = 0;
-    if (big) {
+    if (pt.inv_u == 0.0) {
       S.appr[w] = __longlong_as_double(0x7FF0000000000000ll);  // unknown: forces the slow path if it matters
       S.bnd[w] = 0.0;
+    } else if (big) {
+      // some lanes' fp64 accumulators passed 2^51: their sums are approximate, each off by at
+      // most (terms summed) * 2^-53 * (their sum of |R|), and so is every later add (wave tree,
+      // LDS atomics); the reference's own sequential rounding and the per-term rint as below
+      const double u = pt.u, len = (double)W.len;
+      const double qt = (double)A + S.Qd[w];
+      const double smax = fabs(pt.N) + (qt + len) * u;
+      S.appr[w] = pt.N + ((double)Ssum + S.Pd[w]) * u;
+      S.bnd[w] = 2.0 * (len * u + len * 4.440892098500626e-16 * smax) + 2.0 * (len + 256.0) * 2.220446049250313e-16 * qt * u +
+                 1e-300;
     } else {
       const double u = pt.u, len = (double)W.len;
       const double smax = fabs(pt.N) + ((double)A + len) * u;
@@ -872,7 +918,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
 #endif
   walk_bounds_par(S, P, tid, nw);
   if (tid < nw) {
-    S.P[tid] = 0; S.Q[tid] = 0; S.wflag[tid] = 0; S.need_slow[tid] = 0;
+    S.P[tid] = 0; S.Q[tid] = 0; S.Pd[tid] = 0.0; S.Qd[tid] = 0.0; S.wflag[tid] = 0; S.need_slow[tid] = 0;
     for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = 0;
   }
   if (tid == 0) S.n_ties = 0;
@@ -1053,9 +1099,14 @@ __device__ __forceinline__ int argmax_or_mark(Smem& S, int first, int count, dou
   double bv = prior_val;
   for (int c = first; c < first + count; c++)
     if (S.exact[c] && S.val[c] > bv) { bi = c; bv = S.val[c]; }
+  // the best lower bound, inexact candidates included: a candidate whose upper bound is below
+  // it cannot be the maximum (only the rest need their exact value)
+  double lb = bv;
+  for (int c = first; c < first + count; c++)
+    if (!S.exact[c] && S.appr[c] - S.bnd[c] > lb) lb = S.appr[c] - S.bnd[c];
   int amb = 0;
   for (int c = first; c < first + count; c++)
-    if (!S.exact[c] && !(S.appr[c] + S.bnd[c] < bv)) { S.need_slow[c] = 1; amb = 1; }
+    if (!S.exact[c] && !(S.appr[c] + S.bnd[c] < lb)) { S.need_slow[c] = 1; amb = 1; }
   return amb ? AMBIG : bi;
 }
 
