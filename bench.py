@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--chromosomes", type=int, default=None,
+                    help="chromosomes per GPU (default: the config's; development aid)")
     ap.add_argument("--genome-scale", type=int, default=1,
                     help="development: chromosomes per rank (>1 rehearses the host load of a larger job on one GPU)")
     ap.add_argument("--traffic-summary", default=None,
@@ -89,6 +91,8 @@ def main() -> int:
     fscl_amd.set_device(device)
 
     cfg = dict(synth.CONFIGS[args.config])
+    if args.chromosomes:
+        cfg["n_chr"] = args.chromosomes
     n_permute = cfg["n_permute"] if args.n_permute is None else args.n_permute
     wd = Path(args.workdir or tempfile.mkdtemp(prefix="fscl_bench_"))
     wd.mkdir(parents=True, exist_ok=True)

@@ -685,6 +685,13 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
       ad[u] = absdist(pv[u], usweep);
       far = far && (ad[u] - 0x1000000u < (uint32_t)P.lt_span);
     }
+#ifdef FSCLG_EXP_LOGLDS  // timing ablation only (wrong results): every log distance from LDS
+    if (LDS) {
+      const double* lt2 = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt);
+#pragma unroll
+      for (int u = 0; u < U; u++) x[u] = lt2[256 + ((ad[u] >> 8) & 255)] + la;
+    } else
+#endif
     if (LDS && __builtin_amdgcn_ballot_w64(far) == ~0ull) {
       const double* lt2 = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt);  // pre-offset by -256 entries
 #pragma unroll

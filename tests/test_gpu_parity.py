@@ -241,3 +241,29 @@ def test_c2_scale_scan_and_short_permutation(built, tmp):
     assert len(pts) == 2000
     assert_rows_equal(points_rows(pts), read_dump(tmp / "o.dump"), "C2")
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+
+
+@pytest.mark.parametrize("name,gen,opts", [
+    # BASELINE config 3 at full size: ascertainment K=2 of M=20, 30 % folded sites
+    ("C3", dict(n_chr=1, chr_len=200_000_000, snps_per_chr=100_000, n=100, folded=0.3, seed=3, sweeps_per_chr=2),
+     ["--asc-depth=20", "--asc-minimum-freq=2", "--n-permute=2"]),
+    # one chromosome of BASELINE config 5 (227k SNPs, n=400): every point's window is a
+    # proper 2*81920+1-SNP window of the chromosome (per-window null sums on the device)
+    ("C5_chr", dict(n_chr=1, chr_len=227_272_727, snps_per_chr=227_273, n=400, seed=5, sweeps_per_chr=2),
+     ["--n-permute=1"]),
+    # BASELINE config 4's genome shape at a quarter of the chromosomes (n=200, 45 Mb each)
+    ("C4_part", dict(n_chr=6, chr_len=45_454_545, snps_per_chr=45_455, n=200, seed=4, sweeps_per_chr=2),
+     ["--n-permute=2"]),
+])
+def test_full_size_configs_match_oracle(built, tmp, name, gen, opts):
+    """Full-size BASELINE workloads beside C2: initial scan plus a short permutation test,
+    bit-exact against the oracle (positions, windows, lalpha, sm_logl, CLR, counts)."""
+    snp = tmp / f"{name}.snp"
+    synth.write_snp_file(str(snp), synth.generate(**gen))
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    fscl_amd.reset_stats()
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), name)
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+    if name == "C5_chr":
+        assert fscl_amd.get_stats()["window_ms"] > 0
