@@ -1224,6 +1224,10 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
   // (round-robin over the XCDs), so the long cells start first and spread over the XCDs
   const int cell = blockIdx.x;
   if (cell >= P.n_cells) return;
+  if (P.mode == 0 && P.cells[cell].chr < 0) {  // idle block of the host's XCD placement
+    if (P.ctrace && tid < 8) P.ctrace[8 * cell + tid] = 0;
+    return;
+  }
   if (tid < 8) S.cnt[tid] = 0;
   if (tid < 4) S.tph[tid] = 0;
   if (P.ctrace && tid == 0) { P.ctrace[8 * cell] = wall_clock64(); P.ctrace[8 * cell + 2] = __smid(); }
@@ -2098,22 +2102,64 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
   B.order.resize(nu);
   for (int u = 0; u < nu; u++) B.order[u] = u;
   std::stable_sort(B.order.begin(), B.order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
-  if ((r = ensure_io(B, nu))) return r;
+  // XCD-aware placement (MI355X_MICROARCH.md: blocks are dealt round-robin over the 8 XCDs,
+  // so blocks b and b + 8 share one XCD's L2).  With several chromosomes in the launch, each
+  // XCD gets a run of consecutive (chromosome, position) cells of 1/8 of the estimated cost,
+  // longest first within it: a chromosome's site array then sits in one or two L2s instead of
+  // all eight.  Class x takes blocks x, x + 8, ...; a class that runs out leaves idle blocks
+  // (chr = -1).  One chromosome: the plain longest-first order.
+  int nl = nu;
+  {
+    int nchr = 0, last = -1;
+    std::vector<int> loc(nu);
+    for (int u = 0; u < nu; u++) loc[u] = u;
+    std::sort(loc.begin(), loc.end(), [&](int x, int y) {
+      const fsclg_cell_t &a = B.ucells[x], &b = B.ucells[y];
+      return a.chr != b.chr ? a.chr < b.chr : a.start_pos < b.start_pos;
+    });
+    for (int u : loc) if (B.ucells[u].chr != last) { nchr++; last = B.ucells[u].chr; }
+    if (nchr > 1 && nu >= 8 * 32 && !getenv("FSCLG_NO_XCD")) {
+      double tot = 0.0;
+      for (int u = 0; u < nu; u++) tot += cost[u];
+      std::vector<int> cls(nu);
+      double acc = 0.0;
+      for (int u : loc) {
+        cls[u] = std::min(7, (int)((acc + 0.5 * cost[u]) * 8.0 / tot));
+        acc += cost[u];
+      }
+      std::vector<int> lists[8];
+      for (int u : B.order) lists[cls[u]].push_back(u);
+      size_t L = 0;
+      for (auto& l : lists) L = std::max(L, l.size());
+      B.order.assign(8 * L, -1);
+      for (size_t j = 0; j < L; j++)
+        for (int x = 0; x < 8; x++)
+          if (j < lists[x].size()) B.order[8 * j + x] = lists[x][j];
+      nl = (int)(8 * L);
+    }
+  }
+  if ((r = ensure_io(B, nl))) return r;
   if (use_ep) {
     if ((r = ensure_buf(&B.d_ept, &B.ept_cap, ne))) return r;
     if ((r = ensure_pinned(&B.p_epos, &B.pep_cap, ne))) return r;
-    if ((r = ensure_pinned(&B.p_cell_ep, &B.pcep_cap, nu))) return r;
+    if ((r = ensure_pinned(&B.p_cell_ep, &B.pcep_cap, nl))) return r;
   }
   B.upos.resize(nu);
-  for (int k = 0; k < nu; k++) {
-    B.p_cells[k] = B.ucells[B.order[k]];
-    if (use_ep) B.p_cell_ep[k] = B.ucell_ep[B.order[k]];
-    B.upos[B.order[k]] = k;
+  for (int k = 0; k < nl; k++) {
+    const int u = B.order[k];
+    if (u < 0) {  // idle block of the XCD placement
+      B.p_cells[k] = fsclg_cell_t{-1, 0, 0};
+      if (use_ep) B.p_cell_ep[k] = make_int2(0, 0);
+      continue;
+    }
+    B.p_cells[k] = B.ucells[u];
+    if (use_ep) B.p_cell_ep[k] = B.ucell_ep[u];
+    B.upos[u] = k;
   }
   if (use_ep) memcpy(B.p_epos, B.epos.data(), sizeof(int2) * ne);
   // the slot's rows and null sums first
   HIPCHK(hipStreamWaitEvent(B.stream, c->slot[slot].ready, 0), "hipStreamWaitEvent");
-  Params P = make_params(c, B, slot, nu, 0, eval_range, bp_resl);
+  Params P = make_params(c, B, slot, nl, 0, eval_range, bp_resl);
   if (c->hist_pending && P.n_civ > 0) {  // diagnostic builds (FSCLG_IVHIST): per phase key
     const int nh = (c->n_coarse + 2) * c->n_iv;
     if ((r = ensure_buf(&c->d_ivhist, &c->ivhist_n, nh))) return r;
@@ -2131,11 +2177,11 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
     P.ept = B.d_ept; P.cell_ep = B.p_cell_ep;
     c->n_ep_saved += (unsigned long long)(2 * nu - ne);
   }
-  if ((r = launch_blocks(B.stream, P, nu))) return r;
+  if ((r = launch_blocks(B.stream, P, nl))) return r;
   HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
   HIPCHK(hipEventRecord(B.ev2, B.stream), "hipEventRecord");
   B.traced = P.ctrace != nullptr;
-  B.nu = nu;
+  B.nu = nl;
   B.nlaunch = use_ep ? 2 : 1;
   B.pending = true;
   c->slot[slot].users++;
@@ -2180,7 +2226,8 @@ int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
       fclose(f);
     }
   }
-  for (int k = 0; k < nu; k++) c->cell_cost[cell_key(B.p_cells[k])] = B.p_out[k].cost;
+  for (int k = 0; k < nu; k++)
+    if (B.p_cells[k].chr >= 0) c->cell_cost[cell_key(B.p_cells[k])] = B.p_out[k].cost;
   for (int i = 0; i < B.n_cells; i++) out[i] = B.p_out[B.upos[B.uidx[i]]];
   for (int i = 0; i < B.n_cells; i++)
     if (out[i].flags) return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL, "device flag");

@@ -11,6 +11,8 @@ i, k = 0, 0
 while i < raw.size:
     n = int(raw[i]); i += 1
     a = raw[i:i + 8 * n].reshape(n, 8).astype(np.int64); i += 8 * n
+    a = a[a[:, 0] > 0]  # idle blocks of the XCD placement
+    n = len(a)
     t0, t1 = a[:, 0] - a[:, 0].min(), a[:, 1] - a[:, 0].min()
     span = t1.max()
     dur = t1 - t0
