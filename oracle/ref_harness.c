@@ -16,11 +16,16 @@
  * opts: --asc-depth=D --asc-minimum-freq=K --include-invariant --minimum-depth=M
  *       --splines=S --ascbias-background-only --force-neutral-spectrum
  *       --n-permute=N --permute-nbp=X --coarse-grid-spacing=G --sweep-width=W
+ *       --n-threads=T (OpenMP threads over the grid cells; the reference's
+ *       search_maxalpha is reentrant: fscl runs it from its own pthreads)
+ * The scan mode prints the wall time of the initial scan alone (scan_s=) on
+ * stderr: bench.py's cpu_baseline leg times the reference's hot code with it.
  */
 #include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "fscl.h" /* the reference's own header, from -I/root/reference */
 #include "oracle.h"
@@ -66,7 +71,8 @@ int main(int argc, char **argv) {
     if (arg_int(a, "--asc-depth", &o.asc_depth) || arg_int(a, "--asc-minimum-freq", &o.asc_min_freq) ||
         arg_int(a, "--minimum-depth", &o.minimum_depth) || arg_int(a, "--splines", &o.spline_pts) ||
         arg_int(a, "--n-permute", &o.n_permute) || arg_dbl(a, "--permute-nbp", &o.permute_nbp) ||
-        arg_int(a, "--coarse-grid-spacing", &o.large_grid_sp) || arg_dbl(a, "--sweep-width", &o.scan_width_mb))
+        arg_int(a, "--coarse-grid-spacing", &o.large_grid_sp) || arg_dbl(a, "--sweep-width", &o.scan_width_mb) ||
+        arg_int(a, "--n-threads", &o.n_threads))
       continue;
     if (!strcmp(a, "--include-invariant")) o.include_invariant = 1;
     else if (!strcmp(a, "--ascbias-background-only")) o.ascbias_background_only = 1;
@@ -100,7 +106,12 @@ int main(int argc, char **argv) {
     orc_scan_t *os = (orc_scan_t *)s;
     orc_null_model(os, fsp);
     orc_set_maxalpha_hook(ref_maxalpha, sm);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     orc_scan_chromosome(os, NULL, &o, &st);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    fprintf(stderr, "ref_harness: scan_s=%.6f threads=%d\n",
+            (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec), o.n_threads);
     if (o.n_permute > 0) orc_scan_permute(os, NULL, &o, &st);
     orc_scan_output(argv[3], os, 0, o.n_permute, NULL);
     orc_dump_points(argv[4], os);
