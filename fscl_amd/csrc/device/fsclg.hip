@@ -2087,6 +2087,31 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
   }
   const int ne = (int)B.epos.size();
   const bool use_ep = !getenv("FSCLG_NO_DEDUP") && (2 * nu - ne) * 8 >= nu;  // saves >= 1/8 of the endpoint work
+  // XCD placement of the endpoint launch (two endpoints per block, blocks dealt round-robin
+  // over the XCDs): in (chromosome, position) order, the blocks x, x + 8, ... of class x take
+  // one consecutive run of endpoints, as the cells below
+  if (use_ep && ne >= 16 * 32 && !getenv("FSCLG_NO_XCD")) {
+    int nchr = 0, last = -1;
+    std::vector<int> loc(ne);
+    for (int e = 0; e < ne; e++) loc[e] = e;
+    std::sort(loc.begin(), loc.end(), [&](int x, int y) {
+      return B.epos[x].x != B.epos[y].x ? B.epos[x].x < B.epos[y].x : B.epos[x].y < B.epos[y].y;
+    });
+    for (int e : loc) if (B.epos[e].x != last) { nchr++; last = B.epos[e].x; }
+    if (nchr > 1) {
+      const int nb = (ne + 1) / 2;
+      std::vector<int> to(ne);
+      int k = 0;
+      for (int x = 0; x < 8; x++)
+        for (int b = x; b < nb; b += 8)
+          for (int h = 0; h < 2; h++)
+            if (2 * b + h < ne) to[loc[k++]] = 2 * b + h;  // only the last block can hold one
+      std::vector<int2> ep2(ne);
+      for (int e = 0; e < ne; e++) ep2[to[e]] = B.epos[e];
+      B.epos.swap(ep2);
+      for (int u = 0; u < nu; u++) B.ucell_ep[u] = make_int2(to[B.ucell_ep[u].x], to[B.ucell_ep[u].y]);
+    }
+  }
   // longest first: each cell's cost in its last launch (permutation trials repeat the cells),
   // else a guess (cells nearer the middle of a chromosome walk further on both sides)
   std::vector<double> cost(nu);
