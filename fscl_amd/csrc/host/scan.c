@@ -526,7 +526,13 @@ typedef struct {
   fsclg_cell_t *cells;
   fsclg_point_t *out;
   int submitted;
+  int lo, hi;             /* this rank's share, fixed at submission */
 } trial_batch_t;
+
+/* per scan point: its permutation cell's cost in the last trial that evaluated it
+   (snp_likelihood terms / 1024, from the exchanged results, so identical on every rank);
+   0 = not yet measured */
+static double *g_pcost;
 
 static void tb_reserve(trial_batch_t *b, int n) {
   if (n <= b->cap) return;
@@ -538,38 +544,45 @@ static void tb_reserve(trial_batch_t *b, int n) {
 
 static void tb_free(trial_batch_t *b) { free(b->pt); free(b->cells); free(b->out); memset(b, 0, sizeof *b); }
 
-/* this rank's contiguous share of a batch (a cell's work scales with its window) */
+/* this rank's contiguous share of a batch by cost: a point's measured cell cost from its
+   last trial, else its window size (~32 terms / 1024 per window site) */
 static void tb_share(const trial_batch_t *b, int eval_range, int *lo, int *hi) {
   double *cost;
   int i;
   *lo = 0; *hi = b->n;
   if (D.world <= 1) return;
   cost = fh_malloc(sizeof(double) * (b->n ? b->n : 1), "cost");
-  for (i = 0; i < b->n; i++)
-    cost[i] = (double)(D.chr_n[b->cells[i].chr] < 2 * eval_range + 1 ? D.chr_n[b->cells[i].chr] : 2 * eval_range + 1);
+  for (i = 0; i < b->n; i++) {
+    const int w = D.chr_n[b->cells[i].chr] < 2 * eval_range + 1 ? D.chr_n[b->cells[i].chr] : 2 * eval_range + 1;
+    cost[i] = g_pcost && g_pcost[b->pt[i]] > 0 ? g_pcost[b->pt[i]] : w / 32.0;
+  }
   rank_share(cost, b->n, lo, hi);
   free(cost);
 }
 
 static void tb_submit(trial_batch_t *b, int slot, int eval_range, int bp_resl) {
-  int lo, hi;
-  tb_share(b, eval_range, &lo, &hi);
+  tb_share(b, eval_range, &b->lo, &b->hi);
   if (D.world > 1) memset(b->out, 0, sizeof(fsclg_point_t) * b->n);
-  dev_check(fsclg_search_submit(D.ctx, b->batch, slot, b->cells + lo, hi - lo, eval_range, bp_resl), "search submit");
+  dev_check(fsclg_search_submit(D.ctx, b->batch, slot, b->cells + b->lo, b->hi - b->lo, eval_range, bp_resl),
+            "search submit");
   b->submitted = 1;
-  D.st.gp_evals += (unsigned long long)(hi - lo);
+  D.st.gp_evals += (unsigned long long)(b->hi - b->lo);
 }
 
 /* wait for a batch and file each result in its point's queue */
 static void tb_wait(trial_batch_t *b, pqueue_t *pq, int eval_range) {
-  int lo, hi, k;
+  int k;
   double tw = fh_now();
+  (void)eval_range;
   if (!b->submitted) return;
-  tb_share(b, eval_range, &lo, &hi);
-  dev_check(fsclg_search_wait(D.ctx, b->batch, b->out + lo), "search wait");
+  dev_check(fsclg_search_wait(D.ctx, b->batch, b->out + b->lo), "search wait");
   b->submitted = 0;
   D.st.wait_s += fh_now() - tw;
-  if (D.world > 1) exchange((long long *)b->out, (int)(b->n * (sizeof(fsclg_point_t) / sizeof(long long))));
+  if (D.world > 1) {
+    exchange((long long *)b->out, (int)(b->n * (sizeof(fsclg_point_t) / sizeof(long long))));
+    if (g_pcost)
+      for (k = 0; k < b->n; k++) g_pcost[b->pt[k]] = (double)b->out[k].cost;
+  }
   for (k = 0; k < b->n; k++) {
     pqueue_t *q = pq + b->pt[k];
     int j;
@@ -623,6 +636,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   for (k = 0; k < K; k++) { Bt[k].batch = 2 + k; nul[k] = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums"); }
   act = fh_malloc(sizeof(int) * (n_act ? n_act : 1), "active points");
   pq = fh_calloc(n_act ? n_act : 1, sizeof(pqueue_t), "result queues");
+  if (D.world > 1) g_pcost = fh_calloc(n_act ? n_act : 1, sizeof(double), "point costs");
   tb_reserve(&A, n_act ? n_act : 1);
   for (k = 0; k < K; k++) tb_reserve(&Bt[k], n_act ? n_act : 1);
   for (i = 0; i < n_act; i++) act[i] = i;
@@ -724,6 +738,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   tb_free(&A);
   for (k = 0; k < K; k++) { tb_free(&Bt[k]); free(nul[k]); }
   free(act); free(pq);
+  free(g_pcost); g_pcost = NULL;
 }
 
 /* scan-chromosome.c:582-652 (with --n-threads=1 pruning semantics) */
