@@ -649,7 +649,6 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
   const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
   const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
   int civ = 0;
-  double tlo = __builtin_inf(), thi = -__builtin_inf();  // empty: the first trip takes the per-lane path
   double sum = 0.0, mag = 0.0;
 #ifndef FSCLG_NO_PF
   // the sites of the next trip are loaded one trip ahead (nx), issued after the trip's own
@@ -703,9 +702,10 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
     if (kb == 0) {  // a segment's first trip: centre the interval on its last site
       const double xl = readlane_f64(x[U - 1], 63);
       civ = __builtin_amdgcn_readfirstlane(interval_of<LDS>(xl, S, P));
-      tlo = uniform_f64(thrp[civ]);
-      thi = uniform_f64(thrp[civ + 1]);
     }
+    // the bounds of civ, read afresh each trip (a broadcast LDS read): carried across trips
+    // they cost four 64-bit register copies per trip at the loop's phi
+    const double tlo = thrp[civ], thi = thrp[civ + 1];
     // one ballot per compare (SGPR masks, no bool materialised per lane)
     unsigned long long inm = ~0ull;
 #pragma unroll
@@ -737,8 +737,6 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
       int iv[U];
       coef_stage<LDS>(x, rv, S, P, ivc0, ca, cb, iv);
       civ = __builtin_amdgcn_readlane(iv[U - 1], 63);  // the trip's last site
-      tlo = uniform_f64(thrp[civ]);
-      thi = uniform_f64(thrp[civ + 1]);
     }
     double nul[U];
 #pragma unroll
