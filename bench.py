@@ -180,7 +180,7 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded neutral-spectrum SNPs with planted sweeps, fscl_amd/synth.py)",
-        "config": {"workload": f"{args.config}: {world * args.genome_scale} x ({cfg['snps_per_chr']} SNPs, {cfg['chr_len'] // 10**6} Mb, "
+        "config": {"workload": f"{args.config}: {cfg['n_chr'] * world * args.genome_scale} x ({cfg['snps_per_chr']} SNPs, {cfg['chr_len'] // 10**6} Mb, "
                                f"n={cfg['n']}) chromosome(s), G=100kb, {n_permute} permutations, parity mode",
                    "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"] * world * args.genome_scale,
                    "units_per_step": units / args.steps},
