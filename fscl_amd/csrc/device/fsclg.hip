@@ -59,11 +59,11 @@ namespace {
 constexpr int WG = FSCLG_WG;
 constexpr int NWAVE = WG / 64;
 #ifndef FSCLG_SEG
-#define FSCLG_SEG 2048
+#define FSCLG_SEG 4096
 #endif
 constexpr int SEG = FSCLG_SEG;     // terms per work segment
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
-constexpr int MAXSEG_W = (163841 / SEG + 2 + 31) / 32 * 32;  // segments per walk (82 at 163841 terms)
+constexpr int MAXSEG_W = (163841 / SEG + 2 + 31) / 32 * 32;  // segments per walk (42 at 163841 terms)
 constexpr int SEGWORDS = MAXSEG_W / 32;
 constexpr int MAXTIES = 512;       // per eval_walks; overflow sends the affected argmax to the exact slow path
 constexpr int MAXREF = 16;
