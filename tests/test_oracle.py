@@ -77,6 +77,21 @@ def test_oracle_matches_live_reference(built, tmp, seed, opts):
     assert_rows_equal(read_dump(tmp / "o.dump"), read_dump(tmp / "r.dump"), f"seed {seed}")
 
 
+@pytest.mark.skipif(not HARNESS.exists(), reason="needs /root/reference (oracle/_ref)")
+def test_reference_harness_threads_do_not_change_results(built, tmp):
+    """bench.py times the reference's own search_maxalpha on OpenMP threads (its
+    cpu_baseline leg): the threaded harness gives the single-threaded results."""
+    c = manifest()["cases"]["g1_p25"]
+    outs = []
+    for th in (1, 4):
+        r = subprocess.run([str(HARNESS), "scan", str(GOLD / c["input"]), str(tmp / f"h{th}.out"),
+                            str(tmp / f"h{th}.dump"), f"--n-threads={th}"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        assert "scan_s=" in r.stderr
+        outs.append(((tmp / f"h{th}.out").read_bytes(), (tmp / f"h{th}.dump").read_bytes()))
+    assert outs[0] == outs[1]
+
+
 def test_oracle_cli_rejects_bad_options(built, tmp):
     r = subprocess.run([str(ORACLE), "-o", str(tmp / "x")], capture_output=True, text=True)
     assert r.returncode != 0
