@@ -189,7 +189,11 @@ def main() -> int:
                      "kernel": "search_maxpos_kernel", "alg_bytes_per_launch": alg_bytes / launches,
                      "avg_launch_ms": st["kernel_ms"] / launches, "launches": st["n_launches"],
                      "busy_ms": st["busy_ms"], "terms_per_s": st["n_terms"] / busy_s if busy_s > 0 else 0.0,
-                     "fp64_tflops": fp64, "fp64_frac": fp64 / FP64_PEAK_TFS},
+                     "fp64_tflops": fp64, "fp64_frac": fp64 / FP64_PEAK_TFS,
+                     "note": "achieved = SURVEY 8(d) algorithmic bytes (8 B per SNP term and per window-null "
+                             "element) over the union of the kernel's launches; measured HBM traffic (traffic) is "
+                             "~0.3 % of it: sites, tables and coefficient windows stay in L2/LDS, and the kernel "
+                             "is bound by VALU issue and LDS/L2 latency (DESIGN.md 4.6)"},
         "cpu_baseline": None,
         "max_abs_dclr": None,
         "setup_s": setup_s,
