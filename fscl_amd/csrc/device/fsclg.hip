@@ -889,6 +889,10 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
       S.appr[w] = pt.N + ((double)Ssum + S.Pd[w]) * u;
       S.bnd[w] = 2.0 * (len * u + len * 4.440892098500626e-16 * smax) + 2.0 * (len + 256.0) * 2.220446049250313e-16 * qt * u +
                  1e-300;
+      // a NaN sum has a NaN term (R = rint(t/u) is finite for finite t) or both infinities
+      // among the terms: the sequential sum of sm-search.c is then NaN in any order, and a
+      // NaN never wins the strict '>' of search_maxalpha (NaN spline rows, Q15)
+      if (S.appr[w] != S.appr[w]) { S.exact[w] = 1; S.val[w] = S.appr[w]; }
     } else {
       const double u = pt.u, len = (double)W.len;
       const double smax = fabs(pt.N) + ((double)A + len) * u;
