@@ -1393,6 +1393,8 @@ struct Slot {
   double* h_null = nullptr;       // pinned (coherent) whole-chromosome null sums, n_chr
   int rows_cap = 0, null_cap = 0;
   hipEvent_t ready = nullptr;     // recorded on the upload stream after the slot's last upload
+  hipEvent_t wev0 = nullptr, wev1 = nullptr;  // bracket the slot's last window null-sum launch
+  bool wpend = false;             // its time not yet added to window_ms (read without blocking later)
   int users = 0;                  // batches submitted on this slot and not yet waited for
 };
 
@@ -1570,7 +1572,11 @@ int fsclg_open(int device, fsclg_ctx** out) {
     HIPCHK(hipEventCreate(&B.ev1), "hipEventCreate");
     HIPCHK(hipEventCreateWithFlags(&B.ev2, hipEventDisableTiming), "hipEventCreate");
   }
-  for (int s = 0; s < NSLOT; s++) HIPCHK(hipEventCreateWithFlags(&c->slot[s].ready, hipEventDisableTiming), "hipEventCreate");
+  for (int s = 0; s < NSLOT; s++) {
+    HIPCHK(hipEventCreateWithFlags(&c->slot[s].ready, hipEventDisableTiming), "hipEventCreate");
+    HIPCHK(hipEventCreate(&c->slot[s].wev0), "hipEventCreate");
+    HIPCHK(hipEventCreate(&c->slot[s].wev1), "hipEventCreate");
+  }
   HIPCHK(hipEventCreate(&c->ev_ref), "hipEventCreate");
   HIPCHK(hipEventCreate(&c->wev0), "hipEventCreate");
   HIPCHK(hipEventCreate(&c->wev1), "hipEventCreate");
@@ -1594,6 +1600,8 @@ int fsclg_close(fsclg_ctx* c) {
     for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null}) if (p) hipFree(p);
     for (void* p : {(void*)S.h_rows, (void*)S.h_null}) if (p) hipHostFree(p);
     hipEventDestroy(S.ready);
+    if (S.wev0) hipEventDestroy(S.wev0);
+    if (S.wev1) hipEventDestroy(S.wev1);
   }
   for (Batch& B : c->batch) {
     if (B.d_ept) hipFree(B.d_ept);
@@ -1847,8 +1855,20 @@ static int ensure_io(Batch& B, int n) {
   return FSCLG_OK;
 }
 
+// add a slot's pending window-kernel time to window_ms (blocks only if it is still running)
+static int window_time(fsclg_ctx* c, Slot& S) {
+  if (!S.wpend) return FSCLG_OK;
+  HIPCHK(hipEventSynchronize(S.wev1), "hipEventSynchronize");
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, S.wev0, S.wev1), "hipEventElapsedTime");
+  c->window_ms += ms;
+  S.wpend = false;
+  return FSCLG_OK;
+}
+
 // the null sums of every window of the chromosomes longer than 2*er+1 SNPs, for the slot's
-// rows (window_null_kernel on the upload stream, timed apart from the search)
+// rows (window_null_kernel on the upload stream, timed apart from the search; the host does
+// not wait for it: the slot's batches wait on the GPU, and its time is read later)
 static int ensure_windows(fsclg_ctx* c, int slot, int er) {
   const long long W = 2ll * er + 1;
   Slot& S = c->slot[slot];
@@ -1879,16 +1899,15 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er) {
     c->wtask_er = er;
   }
   if (c->n_wtasks) {
-    HIPCHK(hipEventRecord(c->wev0, c->ustream), "hipEventRecord");
+    int r;
+    if ((r = window_time(c, S))) return r;  // the slot's previous launch (long finished)
+    HIPCHK(hipEventRecord(S.wev0, c->ustream), "hipEventRecord");
     hipLaunchKernelGGL(window_null_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
                        c->d_wtasks, (int)W, S.d_win_null);
     HIPCHK(hipGetLastError(), "launch window_null_kernel");
-    HIPCHK(hipEventRecord(c->wev1, c->ustream), "hipEventRecord");
-    HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
-    HIPCHK(hipEventSynchronize(c->wev1), "hipEventSynchronize");
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, c->wev0, c->wev1), "hipEventElapsedTime");
-    c->window_ms += ms;
+    HIPCHK(hipEventRecord(S.wev1, c->ustream), "hipEventRecord");
+    HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");  // the slot's batches wait for it on the GPU
+    S.wpend = true;
   }
   S.win_er = er;
   S.win_valid = true;
@@ -2320,6 +2339,7 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
   memset(st, 0, sizeof *st);
   st->n_terms = h[0]; st->n_null = h[1]; st->n_walks = h[2]; st->n_maxalpha = h[3];
   st->n_unsafe = h[4]; st->n_slow = h[5]; st->n_ties = h[6]; st->n_cells = h[7];
+  for (int k = 0; k < NSLOT; k++) window_time(c, c->slot[k]);
   st->kernel_ms = c->kernel_ms; st->n_launches = c->launches; st->window_ms = c->window_ms;
   st->n_dup_cells = c->n_dup_cells; st->n_ep_saved = c->n_ep_saved;
   {  // union of the batches' kernel intervals
@@ -2342,6 +2362,7 @@ int fsclg_reset_stats(fsclg_ctx* c) {
   if (!c) return set_err(FSCLG_E_ARG, "stats");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
+  for (int k = 0; k < NSLOT; k++) window_time(c, c->slot[k]);  // pending times belong before the reset
   c->kernel_ms = 0.0; c->launches = 0; c->window_ms = 0.0; c->n_dup_cells = 0; c->n_ep_saved = 0;
   c->busy.clear();
   return FSCLG_OK;
