@@ -157,7 +157,7 @@ def main() -> int:
     # (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), committed under profiles/
     traffic, traffic_src = None, None
     cands = [Path(args.traffic_summary)] if args.traffic_summary else sorted(
-        (ROOT / "profiles").glob("r*_summary.json"))  # round-tagged names sort in round order
+        (ROOT / "profiles").glob(f"r*_{args.config.lower()}_*summary.json"))  # this config's; round tags sort in order
     for q in reversed(cands):
         try:
             t = json.loads(q.read_text()).get("hbm_bytes_per_launch")
