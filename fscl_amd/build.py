@@ -30,8 +30,9 @@ ARCH = os.environ.get("FSCL_AMD_ARCH", "gfx950")
 HOST_SRC = ["util.c", "input.c", "spectrum.c", "tables.c", "scan.c"]
 CFLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-fopenmp", "-Wall", "-Wno-unused-result",
           "-std=gnu11"]
+# iterative-ilp machine scheduling: 0.9 % (C2) / 0.4 % (C4) less time per launch, measured A/B
 HIPFLAGS = [f"--offload-arch={ARCH}", "-O3", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-std=c++17",
-            "-Wno-unused-value", "-Wno-unused-result"]
+            "-Wno-unused-value", "-Wno-unused-result", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 
 
 def _run(cmd: list[str], cwd: Path | None = None) -> None:
@@ -64,7 +65,7 @@ def build_native(force: bool = False, trace: bool = False, variant: str | None =
 
 def _build_native(force: bool, trace: bool, defines: tuple[str, ...] = ()) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
-    hdrs = list((ROOT / "include").glob("*.h")) + [CSRC / "host" / "fscl_host.h"]
+    hdrs = list((ROOT / "include").glob("*.h")) + [CSRC / "host" / "fscl_host.h"] + [Path(__file__)]  # flags live here
     objs = []
     for src in HOST_SRC:
         s = CSRC / "host" / src
