@@ -2,19 +2,22 @@
 """bench.py -- fscl CLR sweep scan + block-permutation test on MI355X.
 
 One step = one whole job of the hot path on resident inputs: the initial scan
-(search_maxpos on every grid cell) plus the permutation test (N+1 lockstep
-trials with pruning), i.e. scan_chromosome + scan_permute of the reference
+(search_maxpos on every grid cell) plus the permutation test (N+1 trials with
+pruning), i.e. scan_chromosome + scan_permute of the reference
 (scan-chromosome.c:228-652).  Input parsing, background spectrum, spline
 tables and the null model are set up once before the timed region.
 
-Workload (BASELINE.json configs[1], "C2"): one synthetic 200 Mb chromosome,
-100k SNPs, n = 100, 2,000 grid cells of 100 kb, 100 permutations.  With
---gpus N (one process per GPU, torch.distributed over RCCL) the genome has N
-such chromosomes (weak scaling); ranks run the same host logic and split the
-cells, with one int64 sum-allreduce per trial (parity mode: bit-identical to
-one GPU).
+Workload (default, BASELINE.json configs[3], "C4" -- the north star's target
+configuration, which fits one GPU): 22 synthetic chromosomes of 45.45 Mb, 1.0M
+SNPs, n = 200, 10,010 grid cells of 100 kb, 1,000 permutations.  --gpus N (one
+process per GPU, launched by torch.distributed.run) strong-scales the SAME job:
+every rank runs the same host logic (rand stream, permutation, pruning) and
+evaluates a cost-balanced contiguous share of every batch of cells; one
+shared-memory all-gather per batch (the library's own, fscl_amd_set_ranks_shm)
+completes the results on every rank (parity mode: bit-identical to one GPU).
+--config C2 gives BASELINE configs[1].
 
-value = (grid points + sum of permute_n) / wall seconds over all ranks.
+value = (grid points + sum of permute_n) / wall seconds (max over ranks).
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -22,9 +25,12 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
+import subprocess
 import sys
 import tempfile
 import time
+import uuid
 from pathlib import Path
 
 import numpy as np
@@ -35,9 +41,9 @@ sys.path.insert(0, str(ROOT))
 METRIC = "grid-points × permutations / sec; max |ΔCLR| vs reference"
 UNIT = "grid-points×permutations/s"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-FP64_PEAK_TFS = 78.6       # FP64 vector
+FP64_PEAK_TFS = 78.6       # MI355X FP64 vector (spec)
+N_SIMD = 256 * 4           # 256 CUs x 4 SIMD-32 (MI355X_MICROARCH.md)
 BYTES_PER_UNIT = 8         # 8 B per SNP-term and per window-null element
-FLOPS_PER_TERM = 20        # ~20 FP64 ops per term
 
 
 def parse():
@@ -45,19 +51,88 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="C2")
+    ap.add_argument("--config", default="C4")
     ap.add_argument("--n-permute", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: every CPU this process may run on)")
+    ap.add_argument("--cpu-sample", type=int, default=None, help="CPU baseline: cells in the sample")
+    ap.add_argument("--exchange", choices=("shm", "torch"), default="shm",
+                    help="multi-process exchange: the library's shared-memory all-gather, or a torch.distributed "
+                         "all-reduce callback")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--chromosomes", type=int, default=None,
-                    help="chromosomes per GPU (default: the config's; development aid)")
-    ap.add_argument("--genome-scale", type=int, default=1,
-                    help="development: chromosomes per rank (>1 rehearses the host load of a larger job on one GPU)")
-    ap.add_argument("--traffic-summary", default=None,
-                    help="rocprofv3 PMC summary (tools/prof_summary.py) for roofline.traffic; default: newest in profiles/")
+                    help="chromosomes (default: the config's; development aid)")
+    ap.add_argument("--profile-summary", default=None,
+                    help="rocprofv3 summary (tools/prof_summary.py) for roofline.traffic and the issue roofline; "
+                         "default: the newest profiles/r*_<config>_*summary.json")
     return ap.parse_args()
+
+
+def cpu_info() -> dict:
+    """The host's CPU model and core counts (CPU-baseline context)."""
+    model, phys = None, set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" in line:
+                k, v = (x.strip() for x in line.split(":", 1))
+                if k == "model name" and model is None:
+                    model = v
+                cur[k] = v
+            elif cur:
+                phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    return {"cpu_model": model or platform.processor(), "node_logical_cpus": os.cpu_count(),
+            "node_physical_cores": len(phys) or None, "affinity_cpus": len(os.sched_getaffinity(0))}
+
+
+def profile_summary(args) -> tuple[dict | None, str | None]:
+    cands = [Path(args.profile_summary)] if args.profile_summary else sorted(
+        (ROOT / "profiles").glob(f"r*_{args.config.lower()}_*summary.json"))  # round tags sort in order
+    for q in reversed(cands):
+        try:
+            d = json.loads(q.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("hbm_bytes_per_launch"):
+            return d, str(q.relative_to(ROOT) if q.is_absolute() else q)
+    return None, None
+
+
+def issue_roofline(prof: dict) -> dict | None:
+    """VALU issue rate of the dominant kernel from the committed rocprofv3 PMC passes alone:
+    wave-instructions per launch (SQ_INSTS_VALU; FP64 ones from the SQ_INSTS_VALU_*_F64
+    counters where collected) weighted by their issue cost on a SIMD-32 (MI355X_MICROARCH.md:
+    a wave64 VALU op 2 cycles, FP64 4), over the SIMD-cycles the launch occupied (the union of
+    the overlapping launches x 1024 SIMDs x the clock GRBM_GUI_ACTIVE / 8 / dispatch time)."""
+    pmc = prof.get("pmc_per_launch", {})
+    tu, tr = prof.get("trace_union"), prof.get("trace")
+    if not (pmc.get("SQ_INSTS_VALU") and tu and tr):
+        return None
+    valu = pmc["SQ_INSTS_VALU"]
+    f64 = sum(v for k, v in pmc.items() if k.startswith("SQ_INSTS_VALU_") and k.endswith("_F64"))
+    f64_src = "SQ_INSTS_VALU_*_F64 counters" if f64 else None
+    if not f64:  # static share of FP64 VALU in the term loop (DESIGN.md §4.6) when not collected
+        f64 = valu * prof.get("fp64_valu_share", 0.5)
+        f64_src = f"static FP64 share {prof.get('fp64_valu_share', 0.5)} of VALU (DESIGN.md §4.6)"
+    clk = pmc.get("GRBM_GUI_ACTIVE", 0) / 8 / (tr["avg_ms"] * 1e-3) if pmc.get("GRBM_GUI_ACTIVE") else 2.4e9
+    cycles_used = 2 * (valu - f64) + 4 * f64
+    cycles_avail = N_SIMD * clk * tu["busy_ms_per_launch"] * 1e-3
+    out = {"bound": "valu-issue", "achieved": cycles_used / (tu["busy_ms_per_launch"] * 1e-3) / 1e12,
+           "peak": N_SIMD * clk / 1e12, "unit": "T SIMD-cycles/s", "frac": cycles_used / cycles_avail,
+           "valu_insts_per_launch": valu, "fp64_valu_per_launch": f64, "fp64_source": f64_src,
+           "clock_ghz": clk / 1e9}
+    if pmc.get("SQ_INSTS_LDS"):
+        out["lds_insts_per_launch"] = pmc["SQ_INSTS_LDS"]
+    if pmc.get("SQ_WAIT_ANY") and pmc.get("SQ_WAVE_CYCLES"):
+        out["wait_any_frac"] = pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
+    return out
 
 
 def main() -> int:
@@ -81,13 +156,17 @@ def main() -> int:
         else:
             dist.init_process_group(backend)
             dev = torch.device("cpu")
+        if args.exchange == "shm":
+            name = [f"/fscl_amd_{uuid.uuid4().hex}" if rank == 0 else None]
+            dist.broadcast_object_list(name, src=0)
+            fscl_amd.set_ranks_shm(rank, world, name[0])
+        else:
+            def allreduce(arr: np.ndarray) -> None:
+                t = torch.from_numpy(arr).to(dev)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                arr[:] = t.cpu().numpy()
 
-        def allreduce(arr: np.ndarray) -> None:
-            t = torch.from_numpy(arr).to(dev)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            arr[:] = t.cpu().numpy()
-
-        fscl_amd.set_ranks(rank, world, allreduce)
+            fscl_amd.set_ranks(rank, world, allreduce)
     fscl_amd.set_device(device)
 
     cfg = dict(synth.CONFIGS[args.config])
@@ -96,10 +175,8 @@ def main() -> int:
     n_permute = cfg["n_permute"] if args.n_permute is None else args.n_permute
     wd = Path(args.workdir or tempfile.mkdtemp(prefix="fscl_bench_"))
     wd.mkdir(parents=True, exist_ok=True)
-    snp = wd / f"{args.config}_x{world}_r{rank}.snp"
-    gen = dict(cfg)
-    gen["n_chr"] = cfg["n_chr"] * world * args.genome_scale  # weak scaling: N x the single-GPU genome
-    synth.write_snp_file(str(snp), synth.generate(seed=args.seed, sweeps_per_chr=2, **gen))
+    snp = wd / f"{args.config}_r{rank}.snp"
+    synth.write_snp_file(str(snp), synth.generate(seed=args.seed, sweeps_per_chr=2, **cfg))
 
     # ---- untimed setup (input and tables reported separately)
     t0 = time.time()
@@ -117,6 +194,7 @@ def main() -> int:
         torch.cuda.synchronize()
 
     def job():
+        fscl_amd.srand()  # every step is the same job (a fresh process's rand stream, fscl.c:135)
         fscl_amd.scan_chromosome(scan, tab)
         n_gp = scan.contents.n_scan_pts
         if n_permute > 0:
@@ -129,11 +207,11 @@ def main() -> int:
     fscl_amd.reset_stats()
     barrier()
     t0 = time.perf_counter()
-    units, gp = 0, 0
+    units, gp, n_perm_units = 0, 0, 0
     for _ in range(args.steps):
         n_gp, n_perm, pts = job()
         units += n_gp + n_perm
-        gp = n_gp
+        gp, n_perm_units = n_gp, n_perm
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -142,30 +220,33 @@ def main() -> int:
         elapsed = float(t.item())
     st = fscl_amd.get_stats()
 
-    # ---- roofline of the dominant kernel (search_maxpos_kernel), from HIP events on the streams
-    # it is launched on.  Consecutive trials overlap on the GPU (two batch streams), so the
-    # rate divides by the union of the launches' intervals (busy_ms: overlap counted once);
+    # ---- the dominant kernel (search_maxpos_kernel), from HIP events on the streams it is
+    # launched on.  Consecutive trials overlap on the GPU (several batch streams), so rates
+    # divide by the union of the launches' intervals (busy_ms: overlap counted once);
     # avg_launch_ms is the per-dispatch mean that rocprofv3's kernel stats report.
-    kernel_s = st["kernel_ms"] / 1e3
     busy_s = st["busy_ms"] / 1e3
     launches = max(1, st["n_launches"])
     alg_bytes = BYTES_PER_UNIT * (st["n_terms"] + st["n_null"])
-    achieved = alg_bytes / busy_s / 1e9 if busy_s > 0 else 0.0
-    fp64 = FLOPS_PER_TERM * st["n_terms"] / busy_s / 1e12 if busy_s > 0 else 0.0
-
-    # HBM traffic per launch of the same kernel from separate rocprofv3 --pmc passes
-    # (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), committed under profiles/
-    traffic, traffic_src = None, None
-    cands = [Path(args.traffic_summary)] if args.traffic_summary else sorted(
-        (ROOT / "profiles").glob(f"r*_{args.config.lower()}_*summary.json"))  # this config's; round tags sort in order
-    for q in reversed(cands):
-        try:
-            t = json.loads(q.read_text()).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            continue
-        if t:
-            traffic, traffic_src = float(t), str(q.relative_to(ROOT) if q.is_absolute() else q)
-            break
+    alg_gbs = alg_bytes / busy_s / 1e9 if busy_s > 0 else 0.0
+    prof, prof_src = profile_summary(args)
+    traffic = prof.get("hbm_bytes_per_launch") if prof else None
+    roof = issue_roofline(prof) if prof else None
+    if roof is None:  # no committed PMC for this config: the algorithmic-byte figure alone
+        roof = {"bound": "unmeasured", "achieved": alg_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": alg_gbs / HBM_PEAK_GBS}
+    roof.update({
+        "traffic": traffic, "source": prof_src, "kernel": "search_maxpos_kernel",
+        "alg_bytes_per_launch": alg_bytes / launches,
+        "alg_gbs": alg_gbs, "alg_frac": alg_gbs / HBM_PEAK_GBS,
+        "traffic_over_alg": (traffic / (alg_bytes / launches)) if traffic and alg_bytes else None,
+        "hbm_frac": (traffic * launches / busy_s / 1e9 / HBM_PEAK_GBS) if traffic and busy_s > 0 else None,
+        "avg_launch_ms": st["kernel_ms"] / launches, "launches": st["n_launches"], "busy_ms": st["busy_ms"],
+        "terms_per_s": st["n_terms"] / busy_s if busy_s > 0 else 0.0,
+        "note": "bound from measurement (DESIGN.md §4.6): the kernel is latency/issue-bound -- achieved/frac = "
+                "VALU issue cycles (committed rocprofv3 PMC, source) over the SIMD-cycles of the launches; "
+                "alg_gbs/alg_frac = SURVEY 8(d)'s algorithmic bytes (8 B per SNP term and per window-null "
+                "element) over the launches' union (live HIP events); traffic = measured HBM bytes per launch "
+                "(FETCH_SIZE x2 + WRITE_SIZE): sites, tables and coefficient windows stay in L2/LDS"})
 
     out = {
         "metric": METRIC,
@@ -176,24 +257,16 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded neutral-spectrum SNPs with planted sweeps, fscl_amd/synth.py)",
-        "config": {"workload": f"{args.config}: {cfg['n_chr'] * world * args.genome_scale} x ({cfg['snps_per_chr']} SNPs, {cfg['chr_len'] // 10**6} Mb, "
-                               f"n={cfg['n']}) chromosome(s), G=100kb, {n_permute} permutations, parity mode",
-                   "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"] * world * args.genome_scale,
-                   "units_per_step": units / args.steps},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "search_maxpos_kernel", "alg_bytes_per_launch": alg_bytes / launches,
-                     "avg_launch_ms": st["kernel_ms"] / launches, "launches": st["n_launches"],
-                     "busy_ms": st["busy_ms"], "terms_per_s": st["n_terms"] / busy_s if busy_s > 0 else 0.0,
-                     "fp64_tflops": fp64, "fp64_frac": fp64 / FP64_PEAK_TFS,
-                     "note": "achieved = SURVEY 8(d) algorithmic bytes (8 B per SNP term and per window-null "
-                             "element) over the union of the kernel's launches; measured HBM traffic (traffic) is "
-                             "~0.3 % of it: sites, tables and coefficient windows stay in L2/LDS, and the kernel "
-                             "is bound by VALU issue and LDS/L2 latency (DESIGN.md 4.6)"},
+        "config": {"workload": f"{args.config}: {cfg['n_chr']} x ({cfg['snps_per_chr']} SNPs, "
+                               f"{cfg['chr_len'] // 10**6} Mb, n={cfg['n']}) chromosome(s), G=100kb, "
+                               f"{n_permute} permutations, parity mode, one job split over {world} GPU(s)",
+                   "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"],
+                   "units_per_step": units / args.steps, "exchange": args.exchange if world > 1 else None},
+        "roofline": roof,
         "cpu_baseline": None,
         "max_abs_dclr": None,
         "setup_s": setup_s,
@@ -204,72 +277,85 @@ def main() -> int:
                                      "n_ep_saved", "wait_s", "n_crit", "n_drain")},
     }
 
-    # ---- CPU baseline, bounded sample = the initial scan of the same genome, on the host cores:
-    # (1) "reference": oracle/_ref/ref_harness -- the reference's own sm-search.c / sm-spline.c /
-    #     background / asc-bias / input code compiled from its sources (every term, every alpha
-    #     search), under oracle.c's restated scan loop (scan-chromosome.c needs GSL headers absent
-    #     here); (2) "port": oracle/oracle.c alone.  Both are checked against the GPU's initial scan.
+    # ---- CPU baseline (rank 0, one GPU): the reference's own compiled hot path
+    # (oracle/_ref/ref_harness: sm-search.c / sm-spline.c / background / asc-bias / input
+    # compiled from its sources, under oracle.c's restated scan loop -- scan-chromosome.c
+    # needs GSL headers absent here), timed on this host's cores on a bounded sample of the
+    # same job: evenly spread scan cells, one block permutation, and those cells'
+    # permutation-trial cells; the whole job's CPU time is extrapolated from the per-cell
+    # times and the job's own counts.  Then the GPU's initial scan is checked against the
+    # reference code's on a spread sample of cells... and against the oracle on all cells.
     # Test infrastructure: timed and compared here, never called by the product.
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import subprocess
-        sys.path.insert(0, str(ROOT / "oracle"))
-        from oracle import OracleScan  # noqa: E402
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        fscl_amd.scan_chromosome(scan, tab)  # the GPU's initial scan of the same genome
-        gpu = fscl_amd.points(scan)
-
-        def compare(ref):  # ref: [(chr, sweep_pos, clr)] in output order
-            assert len(ref) == len(gpu)
-            d = max((abs(c - g) for (_, _, c), g in zip(ref, gpu["clr"])), default=0.0)
-            m = sum(1 for (ch, p, _), g in zip(ref, gpu) if (ch, p) != (int(g["chr"]), int(g["sweep_pos"])))
-            return d, m
-
-        orc = OracleScan(snp, threads=threads, asc_depth=cfg.get("asc_depth", 0), asc_min_freq=cfg.get("asc_min_freq", 1))
-        t0 = time.perf_counter()
-        orc.scan()
-        port_s = time.perf_counter() - t0
-        port = orc.clr()
-        d_port, m_port = compare(port)
-        port_bl = {"value": len(port) / port_s, "unit": UNIT, "cores": threads, "kind": "port",
-                   "sample": f"initial scan of the same genome ({len(port)} grid points), oracle/oracle.c "
-                             f"with {threads} OpenMP threads, {port_s:.2f} s"}
-        harness = ROOT / "oracle" / "_ref" / "ref_harness"
-        ref_bl = None
-        if harness.exists():
-            hopts = [f"--n-threads={threads}"]
-            if cfg.get("asc_depth", 0):
-                hopts += [f"--asc-depth={cfg['asc_depth']}", f"--asc-minimum-freq={cfg.get('asc_min_freq', 1)}"]
-            r = subprocess.run([str(harness), "scan", str(snp), str(wd / "ref.txt"), str(wd / "ref.dump"), *hopts],
-                               capture_output=True, text=True)
-            scan_s = [float(w.split("=")[1]) for w in r.stderr.split() if w.startswith("scan_s=")]
-            if r.returncode == 0 and scan_s:
-                rows = []
-                for line in (wd / "ref.dump").read_text().splitlines():
-                    f = line.split("\t")
-                    rows.append((int(f[0]), int(f[1]), float.fromhex(f[2])))
-                d_ref, m_ref = compare(rows)
-                ref_bl = {"value": len(rows) / scan_s[0], "unit": UNIT, "cores": threads, "kind": "reference",
-                          "sample": f"initial scan of the same genome ({len(rows)} grid points): the reference's own "
-                                    f"search_maxalpha/sm_likelihood/spline code compiled from its sources "
-                                    f"(oracle/_ref) under the restated scan loop, {threads} OpenMP threads, "
-                                    f"{scan_s[0]:.2f} s"}
-                out["max_abs_dclr"] = d_ref
-                out["position_mismatches"] = m_ref
-            else:
-                print(f"bench: ref_harness failed ({r.returncode}): {r.stderr[-400:]}", file=sys.stderr)
-        if ref_bl is None:
-            out["cpu_baseline"] = port_bl
-            out["max_abs_dclr"] = d_port
-            out["position_mismatches"] = m_port
-        else:
-            out["cpu_baseline"] = ref_bl
-            out["cpu_port"] = dict(port_bl, max_abs_dclr=d_port, position_mismatches=m_port)
+        info = cpu_info()
+        out["cpu_baseline"], out["max_abs_dclr"], out["position_mismatches"] = cpu_baseline(
+            args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, n_perm_units, st["trials"] // max(1, args.steps),
+            units / args.steps, elapsed / args.steps)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
     fscl_amd.shutdown()
     return 0
+
+
+def _harness(snp, cfg, threads, n_cells):
+    harness = ROOT / "oracle" / "_ref" / "ref_harness"
+    opts = [f"--n-threads={threads}"]
+    if cfg.get("asc_depth", 0):
+        opts += [f"--asc-depth={cfg['asc_depth']}", f"--asc-minimum-freq={cfg.get('asc_min_freq', 1)}"]
+    r = subprocess.run([str(harness), "sample", str(snp), str(n_cells), *opts], capture_output=True, text=True)
+    kv = dict(w.split("=", 1) for w in r.stderr.split() if "=" in w and w.split("=", 1)[0] in
+              ("sample_cells", "threads", "cell_s", "perm_gen_s", "perm_cells", "perm_cell_s"))
+    if r.returncode != 0 or "cell_s" not in kv:
+        raise RuntimeError(f"ref_harness sample failed ({r.returncode}): {r.stderr[-400:]}")
+    return {k: float(v) for k, v in kv.items()}
+
+
+def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, trials, units, gpu_job_s):
+    """Returns (cpu_baseline dict, max |dCLR|, position mismatches)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from oracle import OracleScan  # noqa: E402
+    threads = args.cpu_threads or info["affinity_cpus"]
+    n_t = args.cpu_sample or max(64, min(gp, 24 * threads))
+    n_1 = max(8, min(gp, 64))
+    smp = _harness(snp, cfg, threads, n_t)
+    one = _harness(snp, cfg, 1, n_1)
+    # per-cell CPU seconds with `threads` threads (wall / cells) and with one; the job's CPU
+    # time: its initial-scan cells, its permutation-trial cells, and one serial block
+    # permutation per trial (scan-chromosome.c:441-456 runs it on one thread)
+    c_scan, c_perm = smp["cell_s"] / smp["sample_cells"], smp["perm_cell_s"] / smp["perm_cells"]
+    job_s = gp * c_scan + perm_units * c_perm + trials * smp["perm_gen_s"]
+    c1_scan, c1_perm = one["cell_s"] / one["sample_cells"], one["perm_cell_s"] / one["perm_cells"]
+    job1_s = gp * c1_scan + perm_units * c1_perm + trials * one["perm_gen_s"]
+    phys = info["node_physical_cores"] or info["node_logical_cpus"]
+    node_s = (gp * c1_scan + perm_units * c1_perm) / phys + trials * one["perm_gen_s"]  # perfect scaling
+    bl = {"value": units / job_s, "unit": UNIT, "cores": threads, "kind": "reference",
+          "sample": f"{smp['sample_cells']:.0f} evenly spread grid cells of the same genome, one block permutation "
+                    f"and those cells' permutation-trial cells, through the reference's own compiled "
+                    f"search_maxalpha (oracle/_ref) on {threads} threads; job time extrapolated: {gp} scan cells x "
+                    f"{c_scan * 1e3:.2f} ms + {perm_units} trial cells x {c_perm * 1e3:.2f} ms + {trials} serial "
+                    f"permutations x {smp['perm_gen_s'] * 1e3:.2f} ms = {job_s:.1f} s",
+          "extrapolated": True, "job_s": job_s,
+          "threads_1": {"value": units / job1_s, "job_s": job1_s, "sample_cells": one["sample_cells"]},
+          "node_linear": {"value": units / node_s, "job_s": node_s, "cores": phys,
+                          "note": "one-thread per-cell time / the node's physical cores (perfect scaling, "
+                                  "an upper bound for the CPU) + the serial permutations"},
+          **info, "gpu_over_cpu": job_s / gpu_job_s, "gpu_over_node_linear": node_s / gpu_job_s}
+    # parity of the GPU's initial scan with the oracle on every cell (same run, same host)
+    fscl_amd.srand()
+    fscl_amd.scan_chromosome(scan, tab)
+    gpu = fscl_amd.points(scan)
+    orc = OracleScan(snp, threads=threads, asc_depth=cfg.get("asc_depth", 0), asc_min_freq=cfg.get("asc_min_freq", 1))
+    orc.scan()
+    ref = orc.clr()
+    assert len(ref) == len(gpu)
+    d = max((abs(c - g) for (_, _, c), g in zip(ref, gpu["clr"])), default=0.0)
+    m = sum(1 for (ch, p, _), g in zip(ref, gpu) if (ch, p) != (int(g["chr"]), int(g["sweep_pos"])))
+    bl["parity"] = "initial scan, every grid point, against oracle/oracle.c (bit-exact restatement pinned by "\
+                   "the reference's own compiled code, tests/test_oracle.py)"
+    return bl, d, m
 
 
 if __name__ == "__main__":

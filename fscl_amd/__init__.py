@@ -24,7 +24,8 @@ __all__ = [
     "lib", "LIB_PATH", "CLI_PATH", "SnpT", "ScanPtT", "ScanT", "ChrLimitsT", "SplineT", "SmPtableT", "Stats",
     "load_snp_input", "load_ms_input", "background_fsp", "compute_sweep_model_tables", "compute_snp_null_model",
     "init_log_table", "scan_chromosome", "scan_permute", "scan_output", "output_background_fs", "points",
-    "get_stats", "reset_stats", "set_device", "set_ranks", "shutdown", "run", "device_count",
+    "get_stats", "reset_stats", "set_device", "set_devices", "set_ranks", "set_ranks_shm", "srand", "shutdown", "run",
+    "device_count", "set_dump_output",
 ]
 
 ROOT = Path(__file__).resolve().parent
@@ -79,7 +80,8 @@ class Stats(C.Structure):  # fscl_amd_stats_t
                 ("cache_cover", C.c_double), ("window_ms", C.c_double), ("host_null_s", C.c_double),
                 ("host_upload_s", C.c_double), ("search_s", C.c_double), ("prune_s", C.c_double),
                 ("n_dup_cells", C.c_ulonglong), ("n_ep_saved", C.c_ulonglong), ("busy_ms", C.c_double),
-                ("wait_s", C.c_double), ("n_crit", C.c_ulonglong), ("n_drain", C.c_ulonglong)]
+                ("wait_s", C.c_double), ("n_crit", C.c_ulonglong), ("n_drain", C.c_ulonglong),
+                ("n_devices", C.c_int)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -94,6 +96,9 @@ EXPORTS = [
     "scan_permute", "scan_output", "ascbias_adjust_background", "ascbias_adjust_expect", "configure_logmsg",
     "logmsg", "cr_logmsg", "fscl_amd_load_ms_input", "fscl_amd_set_device", "fscl_amd_set_ranks",
     "fscl_amd_get_stats", "fscl_amd_reset_stats", "fscl_amd_shutdown", "fscl_amd_partition",
+    "fscl_amd_set_devices", "fscl_amd_n_devices", "fscl_amd_set_ranks_shm", "fscl_amd_srand",
+    "fscl_amd_set_dump_output", "fsclg_host_alloc", "fsclg_host_free", "fsclg_slot_wait",
+    "fsclg_slot_set_rows_host",
     "fsclg_open", "fsclg_close", "fsclg_last_error", "fsclg_device_count", "fsclg_upload_tables",
     "fsclg_upload_snps", "fsclg_set_rows", "fsclg_set_chr_null", "fsclg_set_alpha_grid", "fsclg_search_maxpos",
     "fsclg_search_points", "fsclg_get_stats", "fsclg_reset_stats", "fsclg_interval_thresholds",
@@ -126,6 +131,11 @@ def _load() -> C.CDLL:
         "ascbias_adjust_expect": (None, [P(C.c_double), C.c_int, C.c_int, C.c_int]),
         "configure_logmsg": (None, [C.c_int]),
         "fscl_amd_set_device": (C.c_int, [C.c_int]),
+        "fscl_amd_set_devices": (C.c_int, [P(C.c_int), C.c_int]),
+        "fscl_amd_n_devices": (C.c_int, []),
+        "fscl_amd_set_ranks_shm": (C.c_int, [C.c_int, C.c_int, C.c_char_p]),
+        "fscl_amd_srand": (None, [C.c_uint]),
+        "fscl_amd_set_dump_output": (None, [C.c_char_p, C.c_char_p]),
         "fscl_amd_set_ranks": (C.c_int, [C.c_int, C.c_int, EXCHANGE_FN, C.c_void_p]),
         "fscl_amd_get_stats": (None, [P(Stats)]),
         "fscl_amd_partition": (None, [P(C.c_double), C.c_int, C.c_int, C.c_int, P(C.c_int), P(C.c_int)]),
@@ -247,6 +257,39 @@ def set_device(device: int) -> None:
     get_lib().fscl_amd_set_device(int(device))
 
 
+def set_devices(devices=None, n: int | None = None) -> None:
+    """This process drives several GPUs: ``devices`` (a list of ids) or the first ``n``;
+    ``n=0`` (or nothing given): every visible GPU."""
+    if devices is not None:
+        arr = (C.c_int * len(devices))(*[int(d) for d in devices])
+        r = get_lib().fscl_amd_set_devices(arr, len(devices))
+    else:
+        r = get_lib().fscl_amd_set_devices(None, int(n or 0))
+    if r != 0:
+        raise ValueError("bad device list")
+
+
+def srand(seed: int = 0xFD821A6) -> None:
+    """Restart the process-wide permutation rand() stream (srand, fscl.c:135)."""
+    get_lib().fscl_amd_srand(int(seed))
+
+
+_dump_names = []
+
+
+def set_dump_output(path=None, label=None) -> None:
+    """What a SIGINT during scan_permute writes (the reference reads fscl.c's globals)."""
+    b = (_b(path), _b(label))
+    _dump_names.append(b)  # the C side keeps the pointers
+    get_lib().fscl_amd_set_dump_output(*b)
+
+
+def set_ranks_shm(rank: int, world: int, name: str) -> None:
+    """Multi-process parity mode with the library's own shared-memory exchange (one node)."""
+    if get_lib().fscl_amd_set_ranks_shm(int(rank), int(world), name.encode()) != 0:
+        raise RuntimeError(f"fscl_amd_set_ranks_shm({rank}, {world}, {name!r}) failed")
+
+
 def set_ranks(rank: int, world: int, allreduce_sum_int64=None) -> None:
     """Multi-process parity mode.  ``allreduce_sum_int64(np.ndarray[int64]) -> None``
     must sum the array in place across ranks (torch.distributed over RCCL in
@@ -284,10 +327,12 @@ def run(snp_file=None, output=None, *, ms_file=None, ms_segment_length=0, ms_fol
         permute_nbp=0.1, asc_depth=0, asc_min_freq=1, ascbias_background_only=False, include_invariant=False,
         force_neutral=False, minimum_depth=5, large_grid_sp=100000, scan_width_mb=1.0, max_only=False,
         label=None, eval_range=81920, bp_resl=128, verbosity=1):
-    """The fscl main() pipeline (fscl.c:460-482) in-process; returns the scan_t
+    """The fscl main() pipeline (fscl.c:316-337) in-process; returns the scan_t
     pointer (points(scan) reads the results)."""
     get_lib().configure_logmsg(int(verbosity))
     init_log_table()
+    srand()  # init_options (fscl.c:135): a fresh process's stream
+    set_dump_output(output, label)
     scan = (load_ms_input(ms_file, ms_segment_length, ms_folded) if ms_file else
             load_snp_input(snp_file, include_invariant, minimum_depth))
     fsp = background_fsp(scan, force_neutral, None, include_invariant)

@@ -74,9 +74,6 @@ constexpr int LDS_WG = FSCLG_LDS_WG;  // LDS per workgroup (default: two workgro
 constexpr int U = FSCLG_U;         // terms per lane per loop trip (independent load chains)
 constexpr double LOG_AD_MIN = -20.0;  // fscl.h:79
 constexpr double LOG_AD_MAX = 4.0;    // fscl.h:80
-constexpr int BLK_LOG = 10, BLK = 1 << BLK_LOG;  // row-sorted site blocks (Params.prs)
-constexpr int SORT_MIN = 16 * BLK;    // walks this long use the row-sorted blocks
-constexpr int TIE_FIX = 1 << 25;      // tie record flag: in-segment prefix parity still to compute
 constexpr int PAD = 1024;             // slack after pos/row: a trip may read up to 64*U past a walk's end
 constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsigned order = signed order
 
@@ -84,8 +81,6 @@ enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2 };
 
 struct Params {
   const uint2* pr;             // [n_snps + PAD] (position ^ POS_BIAS, device row = caller's row + 1; 0: zero sentinel)
-  const uint2* prs;            // [blocks * BLK + PAD] the same sites, each aligned BLK-block sorted by row:
-                               // (position ^ POS_BIAS, row | offset in block << 16); null: no sorted path
   const double* logt3;         // [3][65536]: c_b + log_table[i], the three branches of sm-search.c:40-46
   const double* coef;          // [n_iv][2 planes][n_rows + 1][2] (coef_off), device row 0 all zero (sentinel)
   const double* nullrow;       // [n_rows + 1], entry 0 zero
@@ -139,7 +134,6 @@ struct Walk {
   int seg0;       // first global segment id
   int nseg;       // left-part segments then right-part segments (seg_bounds)
   int nsl;        // left-part segments
-  int srt;        // segments are row-sorted blocks (prs)
   int wb;         // LDS coefficient window base for this walk
   double la;
   double xl, xr;  // log(alpha d) at the walk's far ends (the walk's largest x is one of them)
@@ -246,9 +240,6 @@ __device__ __forceinline__ double null_of(uint32_t r, const Smem& S, const Param
 // byte offset of (iv, r) in plane A is (iv * stride) * 32 + r * 16, plane B adds
 // P.pstride = stride * 16; 32-bit offsets (the table is < 4 GiB, checked on upload).
 __device__ __forceinline__ uint32_t coef_off(uint32_t r, int iv, const Params& P) {
-#ifdef FSCLG_EXP_COEFCONST  // timing ablation only (wrong results): one block per interval parity
-  return (uint32_t)(iv & 1) << 4;
-#endif
   return (__umul24((uint32_t)iv, (uint32_t)P.stride) << 5) + (r << 4);
 }
 
@@ -262,11 +253,7 @@ __device__ __forceinline__ void coef_ld(const char* base, uint32_t off, const Pa
 // from the global table otherwise
 template <bool LDS>
 __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, const Params& P, double2& a, double2& b) {
-#ifdef FSCLG_NOCACHE  // experiment: coefficients always from the global table
-  if constexpr (false) {
-#else
   if constexpr (LDS) {
-#endif
     const uint32_t ci = (uint32_t)(iv - S.ivc0);
     const bool hit = ci < (uint32_t)P.n_civ;  // every row is cached
     coef_ld(fsclg_dyn, coef_off(r, (int)min(ci, (uint32_t)P.civ_max), P), P, a, b);
@@ -282,11 +269,7 @@ template <bool LDS>
 __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t (&rv)[U], const Smem& S,
                                            const Params& P, int ivc0, double2 (&ca)[U], double2 (&cb)[U],
                                            int (&iv)[U]) {
-#ifdef FSCLG_NOCACHE
-  constexpr bool CACHE = false;
-#else
   constexpr bool CACHE = LDS;
-#endif
 #pragma unroll
   for (int u = 0; u < U; u++) iv[u] = interval_of<LDS>(x[u], S, P);
   if constexpr (CACHE) {
@@ -473,29 +456,19 @@ __device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, 
 }
 
 // A walk covers the site indices [nearest - nl, nearest + nr]; its left part
-// [nearest - nl, nearest] (walked downwards, sm-search.c:190-228) and right part
-// [nearest + 1, nearest + nr] are cut into separate segments (left ones first), so each
-// part's walk order is monotone in the index.  Index-order walks: SEG-site segments.
-// Row-sorted walks: the part's intersections with the aligned BLK-blocks of prs.
+// [nearest - nl, nearest] (walked downwards, sm-search.c:122-128) and right part
+// [nearest + 1, nearest + nr] are cut into separate SEG-site segments (left ones first), so
+// each part's walk order is monotone in the index.
 __device__ __forceinline__ void seg_bounds(const Walk& W, const Pt& pt, int s, int& ib, int& ie) {
   const int lo = pt.nearest - W.nl, near = pt.nearest, hi = pt.nearest + W.nr;
-  if (!W.srt) {
-    if (s < W.nsl) { ib = lo + s * SEG; ie = min(ib + SEG, near + 1); }
-    else { ib = near + 1 + (s - W.nsl) * SEG; ie = min(ib + SEG, hi + 1); }
-  } else if (s < W.nsl) {
-    const int b = (lo >> BLK_LOG) + s;
-    ib = max(b << BLK_LOG, lo); ie = min((b + 1) << BLK_LOG, near + 1);
-  } else {
-    const int b = ((near + 1) >> BLK_LOG) + (s - W.nsl);
-    ib = max(b << BLK_LOG, near + 1); ie = min((b + 1) << BLK_LOG, hi + 1);
-  }
+  if (s < W.nsl) { ib = lo + s * SEG; ie = min(ib + SEG, near + 1); }
+  else { ib = near + 1 + (s - W.nsl) * SEG; ie = min(ib + SEG, hi + 1); }
 }
 
 // the segment of site index i of the walk
 __device__ __forceinline__ int seg_of(const Walk& W, const Pt& pt, int i) {
   const int lo = pt.nearest - W.nl, near = pt.nearest;
-  if (!W.srt) return i <= near ? (i - lo) / SEG : W.nsl + (i - near - 1) / SEG;
-  return i <= near ? (i >> BLK_LOG) - (lo >> BLK_LOG) : W.nsl + (i >> BLK_LOG) - ((near + 1) >> BLK_LOG);
+  return i <= near ? (i - lo) / SEG : W.nsl + (i - near - 1) / SEG;
 }
 
 __device__ __forceinline__ bool odd_int(double v) { return v - 2.0 * floor(0.5 * v) != 0.0; }
@@ -515,115 +488,7 @@ __device__ __forceinline__ double uniform_f64(double v) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-// one segment of one walk, by one wave: U terms per lane per trip with all loads issued
-// first.  Index order (SORTED = false): the segment's sites in order; lanes past it read
-// the padding.  Row-sorted (SORTED = true): the whole BLK-block of prs (neighbouring lanes
-// share rows, so the coefficient gathers touch few lines); lanes whose site lies outside
-// the segment are masked.  Masked lanes take the zero sentinel row (term exactly 0).
-// Per lane: R = rint(t/u) summed in fp64 into the wave's accumulators for this walk
-// (acc = sum R, accm = sum |R|; exact while accm < 2^51, checked when the wave flushes
-// the walk); the segment's parity bit (for the tie replay) from one ballot.  A tie on the
-// sorted path is recorded with TIE_FIX: its in-segment prefix parity (index order) is
-// computed afterwards (fix_ties).
-template <bool LDS, bool SORTED>
-__device__ __forceinline__ void run_segment(Smem& S, int w, int s, const Params& P, int lane, double& acc, double& accm) {
-#ifdef FSCLG_EXP_NOTERMS  // timing ablation only: skip every term
-  return;
-#endif
-  const Walk& W = S.w[w];
-  const Pt& pt = S.pt[W.p];
-  const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS;
-  const double la = W.la, inv = pt.inv_u;
-  const int lo = pt.nearest - W.nl;
-  int ib, ie;
-  seg_bounds(W, pt, s, ib, ie);
-  const int n = SORTED ? BLK : ie - ib;
-  const uint32_t base = SORTED ? (uint32_t)(ib & ~(BLK - 1)) : (uint32_t)ib;
-  const uint2* src = SORTED ? P.prs : P.pr;
-  const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
-  double sum = 0.0, mag = 0.0;
-#ifdef FSCLG_PREFETCH  // (position, row) of the next trip loaded one trip ahead (PAD covers the overshoot)
-  uint2 nx[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) nx[u] = ld_pr(src, base + (uint32_t)(64 * u + lane));
-#endif
-  for (int kb = 0; kb < n; kb += 64 * U) {
-    uint32_t pv[U], rv[U];
-    int orig[U];
-#ifdef FSCLG_PREFETCH
-    uint2 cur[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      cur[u] = nx[u];
-      nx[u] = ld_pr(src, base + (uint32_t)(kb + 64 * U + 64 * u + lane));
-    }
-#endif
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int k = kb + 64 * u + lane;
-#ifdef FSCLG_PREFETCH
-      const uint2 v = cur[u];
-#else
-      const uint2 v = ld_pr(src, base + (uint32_t)k);
-#endif
-      pv[u] = v.x;
-      if constexpr (SORTED) {
-        orig[u] = (int)base + (int)(v.y >> 16);
-        rv[u] = (orig[u] >= ib && orig[u] < ie) ? (v.y & 0xFFFFu) : 0u;  // zero sentinel row outside
-      } else {
-        orig[u] = ib + k;
-        rv[u] = k < n ? v.y : 0u;  // zero sentinel row past the segment
-      }
-    }
-    double x[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-#ifdef FSCLG_EXP_LTCONST  // timing ablation only (wrong results): the gather hits 8 table entries
-      x[u] = P.logt3[absdist(pv[u], usweep) & 7] + la;
-#else
-      x[u] = logt_lds<LDS>(absdist(pv[u], usweep), P) + la;
-#endif
-    }
-#ifdef FSCLG_IVHIST  // diagnostic: one interval sample per segment, weighted by its terms
-    if (P.ivhist && kb == 0 && lane == 0)
-      atomicAdd(&P.ivhist[S.hkey * P.n_iv + interval_of<LDS>(x[0], S, P)], (unsigned long long)(ie - ib));
-#endif
-    double2 ca[U], cb[U];
-    int ivs[U];
-    coef_stage<LDS>(x, rv, S, P, ivc0, ca, cb, ivs);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
-      const double q = (y - null_of<LDS>(rv[u], S, P)) * inv;
-      const double R = rint(q);                 // the even neighbour at a tie; the resolver settles ties
-      const double fr = q - R;
-      if (__ballot(fabs(fr) == 0.5)) {          // rare: record the tie
-        int pre = 0;
-        if constexpr (!SORTED) {                // in-segment prefix parity: earlier trips, earlier lanes
-          const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-          const unsigned long long ps = __ballot(odd_int(sum));
-          const unsigned long long pr = __ballot(odd_int(R));
-          pre = (__popcll(ps) + __popcll(pr & below)) & 1;
-        }
-        if (fabs(fr) == 0.5) {
-          const int ti = atomicAdd(&S.n_ties, 1);
-          if (ti < MAXTIES)
-            S.ties[ti] = (SORTED ? TIE_FIX : 0) | (w << 20) | ((fr < 0.0 ? 1 : 0) << 19) | (pre << 18) | (orig[u] - lo);
-        }
-      }
-      sum += R;
-      mag += fabs(R);
-    }
-  }
-  // the segment's parity: sum over lanes of (sum mod 2); partials are exact integers
-  // whenever the walk passes its flush check (otherwise its value is discarded)
-  const unsigned long long odd = __ballot(odd_int(sum));
-  if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
-  acc += sum;
-  accm += mag;
-}
-
-// run_segment for index-order segments with a wave-uniform spline interval.  Along a segment
+// one index-order segment of one walk, by one wave, with a wave-uniform spline interval.  Along a segment
 // the sites move monotonically away from (or towards) the sweep, and a trip's 64*U sites
 // usually span a small fraction of one interval, so the wave carries the interval civ of its
 // last site with its exact bounds [thr[civ], thr[civ+1]) in scalar registers: when every
@@ -635,9 +500,6 @@ __device__ __forceinline__ void run_segment(Smem& S, int w, int s, const Params&
 template <bool LDS>
 __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Params& P, int lane, double& acc,
                                                 double& accm) {
-#ifdef FSCLG_EXP_NOTERMS
-  return;
-#endif
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[W.p];
   const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS;
@@ -650,25 +512,19 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
   const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
   int civ = 0;
   double sum = 0.0, mag = 0.0;
-#ifndef FSCLG_NO_PF
   // the sites of the next trip are loaded one trip ahead (nx), issued after the trip's own
   // coefficient loads so that waiting for a global coefficient gather (vmcnt counts in
   // order) does not wait for them; PAD covers the look-ahead past a segment's end
   uint2 nx[U];
 #pragma unroll
   for (int u = 0; u < U; u++) nx[u] = ld_pr(P.pr, (uint32_t)(ib + 64 * u + lane));
-#endif
   auto trip = [&](const int kb, auto maskc) {
     constexpr bool MASK = decltype(maskc)::value;
     uint32_t pv[U], rv[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int k = kb + 64 * u + lane;
-#ifndef FSCLG_NO_PF
       const uint2 v = nx[u];
-#else
-      const uint2 v = ld_pr(P.pr, (uint32_t)(ib + k));
-#endif
       pv[u] = v.x;
       rv[u] = (!MASK || k < n) ? v.y : 0u;  // zero sentinel row past the segment
     }
@@ -684,13 +540,6 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
       ad[u] = absdist(pv[u], usweep);
       far = far && (ad[u] - 0x1000000u < (uint32_t)P.lt_span);
     }
-#ifdef FSCLG_EXP_LOGLDS  // timing ablation only (wrong results): every log distance from LDS
-    if (LDS) {
-      const double* lt2 = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt);
-#pragma unroll
-      for (int u = 0; u < U; u++) x[u] = lt2[256 + ((ad[u] >> 8) & 255)] + la;
-    } else
-#endif
     if (LDS && __builtin_amdgcn_ballot_w64(far) == ~0ull) {
       const double* lt2 = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt);  // pre-offset by -256 entries
 #pragma unroll
@@ -741,7 +590,6 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
     double nul[U];
 #pragma unroll
     for (int u = 0; u < U; u++) nul[u] = null_of<LDS>(rv[u], S, P);
-#ifndef FSCLG_NO_PF
     // after the last use of this trip's rows (so the look-ahead loads into the same
     // registers, no copy at the loop edge), unconditional (the last trip's look-ahead reads
     // the padding; a conditional load would make the waits below conservative at the join)
@@ -749,7 +597,6 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
 #pragma unroll
     for (int u = 0; u < U; u++) nx[u] = ld_pr(P.pr, (uint32_t)(ib + kb + 64 * U + 64 * u + lane));
     __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
@@ -778,28 +625,6 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
   if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
   acc += sum;
   accm += mag;
-}
-
-// the in-segment prefix parity (index order) of the ties found on the sorted path: one
-// wave per tie re-evaluates R = rint(t/u) of the segment's sites before it, with the same
-// arithmetic as run_segment
-template <bool LDS>
-__device__ __forceinline__ void fix_ties(Smem& S, const Params& P, int wave, int lane) {
-  const int nt = __builtin_amdgcn_readfirstlane(S.n_ties < MAXTIES ? S.n_ties : MAXTIES);
-  for (int t = wave; t < nt; t += NWAVE) {
-    const int v = __builtin_amdgcn_readfirstlane(S.ties[t]);
-    if (!(v & TIE_FIX)) continue;
-    const int w = (v >> 20) & 31;
-    const Walk& W = S.w[w];
-    const Pt& pt = S.pt[W.p];
-    const int it = pt.nearest - W.nl + (v & 0x3FFFF);
-    int ib, ie;
-    seg_bounds(W, pt, seg_of(W, pt, it), ib, ie);
-    int par = 0;
-    for (int i = ib + lane; i < it; i += 64) par ^= odd_int(rint(term_dev<LDS>(i, pt.sweep, W.la, S, P) * pt.inv_u));
-    par = __popcll(__ballot(par != 0)) & 1;
-    if (lane == 0) S.ties[t] = (v & ~(TIE_FIX | (1 << 18))) | (par << 18);
-  }
 }
 
 // a wave's share of walk w: int64 totals of sum R and sum |R| into S.P / S.Q.  Exact when
@@ -934,54 +759,6 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   __syncthreads();
   PHASE_MARK(0);
   TRACE("  bounds done: nw=%d w0 len=%d nl=%d nr=%d\n", nw, S.w[0].len, S.w[0].nl, S.w[0].nr);
-#ifdef FSCLG_SERIAL_LAYOUT  // A/B: the layout by thread 0
-  if (tid == 0) {
-    int seg = 0;
-    unsigned long long terms = 0;
-    for (int w = 0; w < nw; w++) {
-      Walk& W = S.w[w];
-      W.len = W.len ? 1 + W.nl + W.nr : 0;
-      // the walk's window: the n_civ intervals below the one of its largest x (the site
-      // count of a long walk grows like e^x up to there)
-      const int K = P.n_civ;
-      W.wb = -1;  // empty walks sort last and open no group
-      if (LDS && K > 0 && W.len) {
-        const int top = interval_of<LDS>(fmax(W.xl, W.xr), S, P);
-        W.wb = min(max(top - K + 1, 0), P.n_iv - K);
-      }
-    }
-    // walks in descending window base; a group shares the window of its first walk and
-    // takes the following walks whose base is at most 2 below it (they lose at most their
-    // two sparsest intervals)
-    for (int w = 0; w < nw; w++) {
-      int k = w;
-      while (k > 0 && S.w[S.word[k - 1]].wb < S.w[w].wb) { S.word[k] = S.word[k - 1]; k--; }
-      S.word[k] = w;
-    }
-    S.ngrp = 0;
-    for (int k = 0; k < nw; k++) {
-      Walk& W = S.w[S.word[k]];
-      if (W.len && (S.ngrp == 0 || W.wb < S.gwb[S.ngrp - 1] - 2)) {
-        S.gwb[S.ngrp] = W.wb; S.gseg[S.ngrp] = seg; S.ngrp++;
-      }
-      W.srt = (P.prs != nullptr && W.len >= SORT_MIN) ? 1 : 0;
-      const int near = S.pt[W.p].nearest, lo = near - W.nl, hi = near + W.nr;
-      if (!W.len) { W.nsl = 0; W.nseg = 0; }
-      else if (!W.srt) { W.nsl = (W.nl + SEG) / SEG; W.nseg = W.nsl + (W.nr + SEG - 1) / SEG; }
-      else {
-        W.nsl = (near >> BLK_LOG) - (lo >> BLK_LOG) + 1;
-        W.nseg = W.nsl + (W.nr ? (hi >> BLK_LOG) - ((near + 1) >> BLK_LOG) + 1 : 0);
-      }
-      W.seg0 = seg;
-      seg += W.nseg;
-      terms += W.len;
-    }
-    S.gseg[S.ngrp] = seg;
-    S.seg_total = seg;
-    S.cnt[0] += terms;
-    S.cnt[2] += nw;
-  }
-#else
   // layout by wave 0, one lane per walk (nw <= MAXWALK = 32), values in registers
   if (wave == 0) {
     const bool act = lane < nw;
@@ -996,16 +773,11 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
         const int top = interval_of<LDS>(fmax(W.xl, W.xr), S, P);
         wb = min(max(top - K + 1, 0), P.n_iv - K);
       }
-      const int srt = (P.prs != nullptr && len >= SORT_MIN) ? 1 : 0;
       const int near = S.pt[W.p].nearest, lo = near - W.nl, hi = near + W.nr;
       int nsl;
       if (!len) { nsl = 0; nseg = 0; }
-      else if (!srt) { nsl = (W.nl + SEG) / SEG; nseg = nsl + (W.nr + SEG - 1) / SEG; }
-      else {
-        nsl = (near >> BLK_LOG) - (lo >> BLK_LOG) + 1;
-        nseg = nsl + (W.nr ? (hi >> BLK_LOG) - ((near + 1) >> BLK_LOG) + 1 : 0);
-      }
-      W.len = len; W.wb = wb; W.srt = srt; W.nsl = nsl; W.nseg = nseg;
+      else { nsl = (W.nl + SEG) / SEG; nseg = nsl + (W.nr + SEG - 1) / SEG; }
+      W.len = len; W.wb = wb; W.nsl = nsl; W.nseg = nseg;
     }
     // walks in descending window base, stable: each walk's rank and first segment
     int rank = 0, seg0 = 0;
@@ -1040,7 +812,6 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
       S.cnt[2] += nw;
     }
   }
-#endif
   __syncthreads();
   PHASE_MARK(1);
   TRACE("  layout done: segs=%d\n", S.seg_total);
@@ -1066,26 +837,12 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
         if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
         cw = w; acc = 0.0; accm = 0.0;
       }
-#ifdef FSCLG_SORTED_PATH
-      if (S.w[w].srt) run_segment<LDS, true>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
-      else
-#endif
-#ifdef FSCLG_LANE_IV  // A/B: per-lane interval on every trip
-      run_segment<LDS, false>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
-#else
       run_segment_idx<LDS>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
-#endif
      }
     }
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
   }
   __syncthreads();
-#ifdef FSCLG_SORTED_PATH
-  if (P.prs) {
-    fix_ties<LDS>(S, P, wave, lane);
-    __syncthreads();
-  }
-#endif
   PHASE_MARK(2);
   TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk(S, tid);
@@ -1453,10 +1210,6 @@ struct fsclg_ctx {
   // snps
   uint2* d_pr0 = nullptr;         // (biased position, device row) with the unpermuted rows
   std::vector<uint2> h_pr0;
-  uint2* d_prs = nullptr;         // row-sorted BLK-blocks of slot 0's rows (null: no sorted path)
-  uint2* d_prs0 = nullptr;
-  std::vector<uint2> h_prs;
-  std::vector<int> h_cnt;
   int n_snps = 0;
   int32_t* d_chr_start = nullptr;
   int32_t* d_chr_n = nullptr;
@@ -1469,7 +1222,6 @@ struct fsclg_ctx {
   int lt_hi = 0;                        // logt3 branch-2 entries [256, lt_hi) staged in LDS
   std::vector<long long> h_row_cnt;     // sites per device row
   std::vector<double> h_lt3;
-  std::vector<uint2> h_stage;
   Slot slot[NSLOT];
   Batch batch[NBATCH];
   // LDS coefficient cache plan (fsclg_plan_cache)
@@ -1531,26 +1283,6 @@ static double interval_threshold(int j, double step) {
   return dval(hi);
 }
 
-// each aligned BLK-block of sites sorted by device row (counting sort, stable), entries
-// (biased position, row | offset in block << 16); the tail of the last block points past
-// the sites (masked by every segment)
-static void sort_blocks(fsclg_ctx* c, const uint2* pr) {
-  const int n = c->n_snps, nb = (n + BLK - 1) / BLK, nk = c->n_rows + 1;
-  c->h_prs.assign((size_t)nb * BLK + PAD, make_uint2(POS_BIAS, 0u));
-  c->h_cnt.assign(nk + 1, 0);
-  for (int b = 0; b < nb; b++) {
-    const int b0 = b * BLK, m = std::min(BLK, n - b0);
-    std::fill(c->h_cnt.begin(), c->h_cnt.end(), 0);
-    for (int k = 0; k < m; k++) c->h_cnt[pr[b0 + k].y + 1]++;
-    for (int r = 0; r < nk; r++) c->h_cnt[r + 1] += c->h_cnt[r];
-    for (int k = 0; k < m; k++) {
-      const uint2 v = pr[b0 + k];
-      c->h_prs[b0 + c->h_cnt[v.y]++] = make_uint2(v.x, v.y | ((uint32_t)k << 16));
-    }
-    for (int k = m; k < BLK; k++) c->h_prs[b0 + k] = make_uint2(POS_BIAS, (uint32_t)k << 16);
-  }
-}
-
 extern "C" {
 
 const char* fsclg_last_error(void) { return g_err; }
@@ -1603,7 +1335,7 @@ int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
   hipSetDevice(c->device);
   hipDeviceSynchronize();
-  void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0, c->d_prs, c->d_prs0,
+  void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0,
                   c->d_chr_start, c->d_chr_n, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine,
                   c->d_stats};
   for (void* p : ptrs) if (p) hipFree(p);
@@ -1701,23 +1433,6 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
     HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   }
   c->n_snps = n_snps;
-  // row-sorted blocks: fewer cache lines per coefficient gather, but measured slower once the
-  // coefficient windows follow the walks (the texture data path is bound by bytes, not
-  // lines); kept as an option for slot 0 (FSCLG_SORTED=1), parity-tested
-#ifdef FSCLG_SORTED_PATH
-  const bool sorted_path = true;
-#else
-  const bool sorted_path = false;
-#endif
-  if (sorted_path && c->n_rows > 0 && c->n_rows + 1 < 0x10000 && getenv("FSCLG_SORTED")) {
-    sort_blocks(c, pr.data());
-    if ((r = upload(&c->d_prs0, c->h_prs.data(), c->h_prs.size(), c->ustream))) return r;
-    if ((r = upload(&c->d_prs, c->h_prs.data(), c->h_prs.size(), c->ustream))) return r;
-  } else {
-    if (c->d_prs) hipFree(c->d_prs);
-    if (c->d_prs0) hipFree(c->d_prs0);
-    c->d_prs = nullptr; c->d_prs0 = nullptr;
-  }
   if ((r = upload(&c->d_chr_start, chr_start, (size_t)n_chr, c->ustream))) return r;
   if ((r = upload(&c->d_chr_n, chr_n, (size_t)n_chr, c->ustream))) return r;
   c->wtask_er = -1;
@@ -1747,13 +1462,18 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
 // between a kernel's stores and the host's reads after its completion event)
 static constexpr unsigned HOSTMEM = hipHostMallocCoherent | hipHostMallocMapped;
 
+static int ensure_null_staging(fsclg_ctx* c, Slot& S) {
+  if (S.null_cap >= c->n_chr) return FSCLG_OK;
+  if (S.h_null) hipHostFree(S.h_null);
+  S.h_null = nullptr; S.null_cap = 0;
+  HIPCHK(hipHostMalloc((void**)&S.h_null, sizeof(double) * c->n_chr, HOSTMEM), "hipHostMalloc null sums");
+  S.null_cap = c->n_chr;
+  return FSCLG_OK;
+}
+
 static int ensure_row_staging(fsclg_ctx* c, Slot& S) {
-  if (S.null_cap < c->n_chr) {
-    if (S.h_null) hipHostFree(S.h_null);
-    S.h_null = nullptr; S.null_cap = 0;
-    HIPCHK(hipHostMalloc((void**)&S.h_null, sizeof(double) * c->n_chr, HOSTMEM), "hipHostMalloc null sums");
-    S.null_cap = c->n_chr;
-  }
+  int r;
+  if ((r = ensure_null_staging(c, S))) return r;
   if (S.rows_cap >= c->n_snps) return FSCLG_OK;
   if (S.h_rows) hipHostFree(S.h_rows);
   S.h_rows = nullptr; S.rows_cap = 0;
@@ -1796,24 +1516,52 @@ int fsclg_slot_set_rows(fsclg_ctx* c, int slot, const uint32_t* row, const doubl
                      row ? S.h_rows : nullptr, c->d_pr0, c->n_snps, S.d_chr_null, chr_null ? S.h_null : nullptr,
                      c->n_chr);
   HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
-  if (c->d_prs && slot == 0) {  // opt-in row-sorted blocks (diagnostic): built on the host
-    if (!row) {
-      HIPCHK(hipMemcpyAsync(c->d_prs, c->d_prs0, sizeof(uint2) * c->h_prs.size(), hipMemcpyDeviceToDevice, c->ustream),
-             "copy sorted rows");
-    } else {
-      c->h_stage.resize(c->n_snps);
-      for (int i = 0; i < c->n_snps; i++) c->h_stage[i] = make_uint2(c->h_pr0[i].x, row[i] + 1);
-      sort_blocks(c, c->h_stage.data());
-      HIPCHK(hipMemcpyAsync(c->d_prs, c->h_prs.data(), sizeof(uint2) * c->h_prs.size(), hipMemcpyHostToDevice, c->ustream),
-             "copy sorted rows");
-    }
-    HIPCHK(hipStreamSynchronize(c->ustream), "hipStreamSynchronize");  // h_prs is reused
-  }
   HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   return FSCLG_OK;
 }
 
 int fsclg_set_rows(fsclg_ctx* c, const uint32_t* row) { return fsclg_slot_set_rows(c, 0, row, nullptr); }
+
+void* fsclg_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  const hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, HOSTMEM | hipHostMallocPortable);
+  if (e != hipSuccess) { set_err(FSCLG_E_HIP, "hipHostMalloc (portable)", e); return nullptr; }
+  return p;
+}
+
+void fsclg_host_free(void* p) {
+  if (p) hipHostFree(p);
+}
+
+int fsclg_slot_wait(fsclg_ctx* c, int slot) {
+  if (!c) return set_err(FSCLG_E_ARG, "ctx");
+  if (slot < 0 || slot >= NSLOT) return set_err(FSCLG_E_ARG, "slot");
+  Slot& S = c->slot[slot];
+  if (S.users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");
+  return FSCLG_OK;
+}
+
+int fsclg_slot_set_rows_host(fsclg_ctx* c, int slot, const uint32_t* row, const double* chr_null) {
+  if (!c || !c->d_pr0) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  if (!row) return set_err(FSCLG_E_ARG, "rows");
+  if (slot < 0 || slot >= NSLOT) return set_err(FSCLG_E_ARG, "slot");
+  Slot& S = c->slot[slot];
+  if (S.users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  int r;
+  if ((r = ensure_null_staging(c, S))) return r;
+  HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read h_null
+  S.win_valid = false;
+  if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
+  // read straight from the caller's portable pinned rows (one buffer can feed every device)
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((c->n_snps + 1023) / 1024), dim3(256), 0, c->ustream, S.d_pr, row,
+                     c->d_pr0, c->n_snps, S.d_chr_null, chr_null ? S.h_null : nullptr, c->n_chr);
+  HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
+  HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
+  return FSCLG_OK;
+}
 
 int fsclg_set_chr_null(fsclg_ctx* c, const double* chr_null) {
   if (!c || !c->d_pr0 || !chr_null) return set_err(FSCLG_E_STATE, "snps not uploaded");
@@ -1991,7 +1739,7 @@ static void plan_cache(fsclg_ctx* c) {
 static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int eval_range, int bp_resl) {
   const Slot& S = c->slot[slot];
   Params P;
-  P.pr = S.d_pr; P.prs = slot == 0 ? c->d_prs : nullptr; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
+  P.pr = S.d_pr; P.logt3 = c->d_logt; P.coef = c->d_coef; P.nullrow = c->d_null;
   P.thr = c->d_thr; P.n_rows = c->n_rows; P.stride = c->n_rows + 1; P.pstride = P.stride * 16;
   P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step - 1e-9;
   // dynamic LDS: the planned coefficient window, thresholds and null rows
@@ -2024,11 +1772,13 @@ static int launch_blocks(hipStream_t stream, const Params& P, int n) {
   const int dyn = P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   if (stat + dyn <= LDS_WG) {
-    static bool attr = false;
-    if (!attr) {
+    static unsigned long long attr_set = 0;  // per device (bit = device id)
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev), "hipGetDevice");
+    if (dev >= 64 || !(attr_set >> dev & 1ull)) {
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
-      attr = true;
+      if (dev < 64) attr_set |= 1ull << dev;
     }
     hipLaunchKernelGGL(search_maxpos_kernel<true>, dim3(grid), dim3(WG), dyn, stream, P);
   } else

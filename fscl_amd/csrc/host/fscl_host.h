@@ -14,7 +14,7 @@ void *fh_realloc(void *p, size_t n, const char *where);
 double fh_now(void);
 
 /* glibc random_r TYPE_3 stream (the reference draws glibc rand(), seeded by
-   srand(0xFD821A6) at fscl.c:280); own state so ranks and speculation can
+   srand(0xFD821A6) at fscl.c:135); own state so ranks and speculation can
    replay it exactly */
 typedef struct { int32_t r[31]; int f, b; } fh_rand_t;
 void fh_srand(fh_rand_t *g, unsigned seed);
@@ -51,6 +51,13 @@ const double *fh_log_table(void);
 /* the alpha grids of search_maxalpha (sm-search.c:277-295), computed with the
    reference's own floating-point loop */
 int fh_alpha_grid(double *coarse, int max_coarse, double *refine /* [max_coarse][16] */, int32_t *n_refine);
+
+/* multi-process exchange through POSIX shared memory (ranks.c) */
+typedef struct fh_shm fh_shm_t;
+fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap);
+void fh_shm_close(fh_shm_t *m);
+int fh_shm_allgather(fh_shm_t *m, void *buf, size_t item, int n, int lo, int hi);
+int fh_shm_barrier(fh_shm_t *m);
 
 /* ms reader */
 scan_t *fh_load_ms(const char *fname, int segment_length, int folded, int sample_first, int sample_size);

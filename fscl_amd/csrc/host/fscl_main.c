@@ -1,6 +1,6 @@
 /* fscl_main.c -- the `fscl` command line, drop-in for the reference's
- * (option table fscl.c:183-247, defaults :272-323, validation :325-403,
- * main :417-486, parsing cmdline-utils.c:28-100: "--long=value" or
+ * (option table fscl.c:38-102, defaults :127-178, validation :180-258,
+ * main :272-341, parsing cmdline-utils.c:28-100: "--long=value" or
  * "-x value", flags toggle).  The scan path runs on the GPU.
  *
  * Deliberate differences: "--long value" without '=' is an
@@ -18,7 +18,7 @@
 enum { T_STR, T_INT, T_DBL, T_FLAG };
 typedef struct { char s; const char *l; void *v; int t; const char *doc; } opt_t;
 
-/* fscl.c:178-179 */
+/* fscl.c:33-34 */
 char *prepend_label, *output_fname;
 int spline_pts, n_permute;
 
@@ -30,7 +30,7 @@ static void usage(const opt_t *o) {
   }
 }
 
-/* --max-only for ms input: one line per block (fscl.c:213-214) */
+/* --max-only for ms input: one line per block (fscl.c:68-69, :307-308) */
 static void output_block_maxima(const char *fname, scan_t *s, const char *label) {
   FILE *f = fname ? fopen(fname, "w") : stdout;
   int c, i;
@@ -52,7 +52,7 @@ int main(int argc, char **argv) {
   int force_neutral = 0, ms_segment_length = 0, ms_folded = 0, ms_sample_first = 0, ms_sample_size = 0;
   int asc_depth = 0, asc_min_freq = 1, bg_only = 0, include_invariant = 0, maximum_only = 0;
   int small_grid_sp = 1000, large_grid_sp = 100000, dont_scan = 0, minimum_obs_depth = 5, n_threads = 1;
-  int verbosity = MSG_STATUS, eval_range = 81920, bp_resl = 128, stop = 0, i;
+  int verbosity = MSG_STATUS, eval_range = 81920, bp_resl = 128, stop = 0, i, n_gpus = 0;
   double permute_nbp = 0.1, alpha_factor = 1.0, scan_width_mb = 1.0;
   scan_t *s;
   double **fsp;
@@ -84,6 +84,7 @@ int main(int argc, char **argv) {
       {'o', "output-file", &output_fname, T_STR, "output file for scan results"},
       {0, "no-scan", &dont_scan, T_FLAG, "do not scan chromosome, compute background frequency spectrum only"},
       {0, "ascbias-background-only", &bg_only, T_FLAG, "correct for ascertainment bias only in estimating the background site frequency spectrum"},
+      {0, "n-gpus", &n_gpus, T_INT, "GPUs to use (default: every visible GPU, or $FSCL_AMD_DEVICE alone when set)"},
       {0, NULL, NULL, 0, NULL}};
 
   spline_pts = N_SPLINE_KNOTS;
@@ -121,7 +122,7 @@ int main(int argc, char **argv) {
     i += (lng || (opts[j].v && opts[j].t == T_FLAG)) ? 1 : 2;
   }
 
-  /* fscl.c:325-403 */
+  /* fscl.c:180-258 */
   if (verbosity < 0) verbosity = 0;
   configure_logmsg(verbosity);
   if (bg_only) logmsg(MSG_STATUS, "ascertainment bias correction to background site frequency spectrum only\n");
@@ -163,6 +164,7 @@ int main(int argc, char **argv) {
     stop = 1;
   }
   if (large_grid_sp < 1) { logmsg(MSG_ERROR, "Error: coarse grid spacing must be positive.\n"); stop = 1; }
+  if (n_gpus < 0) { logmsg(MSG_ERROR, "Error: --n-gpus must be >= 0.\n"); stop = 1; }
   if (stop) {
     if (verbosity <= MSG_FATAL) logmsg(MSG_FATAL, "Fatal errors have occurred, use -v 1 or greater to see them.\n");
     exit(-1);
@@ -173,7 +175,10 @@ int main(int argc, char **argv) {
   fsp = background_fsp(s, force_neutral, bs_fname, include_invariant);
   if (output_bs_fname) output_background_fs(output_bs_fname, s, fsp);
   if (!dont_scan) {
-    sm_ptable_t *sm = compute_sweep_model_tables(s, fsp, asc_depth, asc_min_freq, bg_only, include_invariant);
+    sm_ptable_t *sm;
+    if ((n_gpus > 0 || !getenv("FSCL_AMD_DEVICE")) && fscl_amd_set_devices(NULL, n_gpus) != 0)
+      logmsg(MSG_FATAL, "fscl: --n-gpus=%d: at most 16 GPUs per process", n_gpus);
+    sm = compute_sweep_model_tables(s, fsp, asc_depth, asc_min_freq, bg_only, include_invariant);
     compute_snp_null_model(s, fsp);
     scan_chromosome(s, sm, eval_range, bp_resl, large_grid_sp, n_threads);
     if (n_permute > 0)

@@ -24,12 +24,38 @@
 #include "fscl_host.h"
 
 #define CLR_NULL_DIST_SAVE 10000 /* scan-chromosome.c:227 */
-#define PERM_SEED 0xFD821A6      /* fscl.c:280 */
+#define PERM_SEED 0xFD821A6      /* fscl.c:135 */
 
-/* fscl.c:178-179 define these; weak so the library links standalone */
+/* fscl.c:33-34 define these; weak so the library links standalone */
 __attribute__((weak)) int n_permute = 0;
 __attribute__((weak)) char *output_fname = NULL;
 __attribute__((weak)) char *prepend_label = NULL;
+
+/* The permutation stream: glibc's rand() seeded once per process (srand(0xFD821A6) in
+   init_options, fscl.c:135), so it continues across scan_permute calls as the reference's
+   does (e.g. the per-block ms loop, fscl.c:296-305).  fscl_amd_srand() restarts it (what
+   a fresh process would see). */
+static fh_rand_t g_rng;
+static int g_rng_seeded = 0;
+
+void fscl_amd_srand(unsigned seed) {
+  fh_srand(&g_rng, seed);
+  g_rng_seeded = 1;
+}
+
+static fh_rand_t *perm_rng(void) {
+  if (!g_rng_seeded) fscl_amd_srand(PERM_SEED);
+  return &g_rng;
+}
+
+/* what the SIGINT dump writes (scan-chromosome.c:553-560 reads fscl.c's globals
+   output_fname / prepend_label; a library caller without fscl.c sets them here) */
+static const char *g_dump_fname = NULL, *g_dump_label = NULL;
+static int g_dump_set = 0;
+
+void fscl_amd_set_dump_output(const char *fname, const char *label) {
+  g_dump_fname = fname; g_dump_label = label; g_dump_set = 1;
+}
 
 /* ----------------------------------------------------------------- log table */
 static double *g_log_table = NULL;
@@ -83,10 +109,22 @@ int fh_alpha_grid(double *coarse, int max_coarse, double *refine, int32_t *n_ref
   return nc;
 }
 
-/* ---------------------------------------------------------- device state */
+/* ---------------------------------------------------------- device state
+   One host process drives n_dev local GPUs (fscl_amd_set_devices; the fscl CLI's
+   --n-gpus), and optionally takes part in a job of `world` such processes (one per GPU,
+   fscl_amd_set_ranks / fscl_amd_set_ranks_shm).  The host logic -- cells, rand stream,
+   block permutation, null sums, pruning -- runs once per process; every batch of cells is
+   split into world * n_dev contiguous shares of equal estimated cost, share
+   rank * n_dev + l evaluated by local device l; the local shares land in one host array,
+   and with several processes one exchange per batch completes it on every rank. */
+#define FH_MAX_DEV 16
+
 typedef struct {
-  fsclg_ctx *ctx;
-  int device;
+  fsclg_ctx *ctx[FH_MAX_DEV];
+  int dev[FH_MAX_DEV];
+  int n_dev;                       /* open contexts (0: not yet opened) */
+  int want_n;                      /* requested local devices: 0 default (one), -1 all visible */
+  int want_dev[FH_MAX_DEV];
   const sm_ptable_t *tab_key;
   const snp_t *snp_key;
   int n_snps_key;
@@ -97,40 +135,58 @@ typedef struct {
   double *nullrow;
   int32_t *chr_start, *chr_n;
   int n_chr;
+  uint32_t *stage[FSCLG_N_SLOTS];  /* one trial's rows, read by every local device (fsclg_host_alloc) */
+  int stage_cap;
   /* ranks */
   int rank, world;
   fscl_amd_exchange_fn xfn;
   void *xctx;
+  fh_shm_t *shm;
+  FILE *sim;                       /* FSCL_AMD_SIM record / replay file (development: scaling rehearsal) */
+  int sim_replay;
   fscl_amd_stats_t st;
 } dev_t_;
-static dev_t_ D = {NULL, -1, NULL, NULL, 0, 0, {0, NULL, NULL, 0, 0}, NULL, NULL, NULL, NULL, NULL, 0,
-                   0, 1, NULL, NULL, {0}};
+static dev_t_ D = {.rank = 0, .world = 1};
 
-int fscl_amd_set_device(int device) {
-  if (D.ctx) { fsclg_close(D.ctx); D.ctx = NULL; D.tab_key = NULL; D.snp_key = NULL; }
-  D.device = device;
+static void dev_close_all(void) {
+  int l, k;
+  for (l = 0; l < D.n_dev; l++) fsclg_close(D.ctx[l]);
+  for (k = 0; k < FSCLG_N_SLOTS; k++) { fsclg_host_free(D.stage[k]); D.stage[k] = NULL; }
+  D.stage_cap = 0;
+  D.n_dev = 0;
+  D.tab_key = NULL; D.snp_key = NULL;
+}
+
+int fscl_amd_set_devices(const int *devices, int n) {
+  int l;
+  if (n > FH_MAX_DEV || n < -1) return -1;
+  dev_close_all();
+  if (n == 0 || n == -1) { D.want_n = -1; return 0; }  /* every visible device */
+  D.want_n = n;
+  for (l = 0; l < n; l++) D.want_dev[l] = devices ? devices[l] : l;
   return 0;
 }
 
+int fscl_amd_set_device(int device) { return fscl_amd_set_devices(&device, 1); }
+
+int fscl_amd_n_devices(void) { return D.n_dev; }
+
 int fscl_amd_set_ranks(int rank, int world, fscl_amd_exchange_fn fn, void *ctx) {
   if (world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return -1;
+  fh_shm_close(D.shm); D.shm = NULL;
   D.rank = rank; D.world = world; D.xfn = fn; D.xctx = ctx;
   return 0;
 }
 
-static void dev_open(void) {
-  int r, dev = D.device;
-  if (D.ctx) return;
-  if (dev < 0) {
-    const char *e = getenv("FSCL_AMD_DEVICE");
-    if (!e) e = getenv("LOCAL_RANK");
-    dev = e ? atoi(e) : 0;
-  }
-  r = fsclg_open(dev, &D.ctx);
-  if (r != FSCLG_OK)
-    logmsg(MSG_FATAL, "fscl_amd: cannot open GPU %d (%s); the scan path runs only on the GPU", dev,
-           fsclg_last_error());
-  D.device = dev;
+int fscl_amd_set_ranks_shm(int rank, int world, const char *name) {
+  const char *e = getenv("FSCL_AMD_SHM_MB");
+  const size_t cap = (size_t)(e && atoi(e) > 0 ? atoi(e) : 64) << 20;
+  if (world < 1 || rank < 0 || rank >= world || !name) return -1;
+  fh_shm_close(D.shm); D.shm = NULL;
+  D.rank = rank; D.world = world; D.xfn = NULL; D.xctx = NULL;
+  if (world == 1) return 0;
+  D.shm = fh_shm_open(rank, world, name, cap);
+  return D.shm ? 0 : -1;
 }
 
 static int dbg(void) {
@@ -144,15 +200,68 @@ static void dev_check(int r, const char *what) {
   if (r != FSCLG_OK) logmsg(MSG_FATAL, "fscl_amd: %s failed: %s (code %d)", what, fsclg_last_error(), r);
 }
 
+/* FSCL_AMD_SIM=record:<file> (one process, all shares) writes every batch's results;
+   FSCL_AMD_SIM=replay:<file>:<world>[:<rank>] runs as one rank of a `world`-process job:
+   it evaluates only its own share and takes the others from the recording (checking its
+   own bit for bit).  Development aid: the time of a W-rank job's rank on one GPU. */
+static void sim_init(void) {
+  static int done = 0;
+  const char *e = getenv("FSCL_AMD_SIM");
+  char path[1024];
+  int w = 1, r = 0;
+  if (done) return;
+  done = 1;
+  if (!e) return;
+  if (sscanf(e, "record:%1023[^:]", path) == 1 && !strncmp(e, "record:", 7)) {
+    D.sim = fopen(path, "wb");
+    D.sim_replay = 0;
+  } else if (!strncmp(e, "replay:", 7) && sscanf(e + 7, "%1023[^:]:%d:%d", path, &w, &r) >= 2) {
+    D.sim = fopen(path, "rb");
+    D.sim_replay = 1;
+    D.world = w; D.rank = r; D.xfn = NULL; D.shm = NULL;
+  }
+  if (!D.sim) logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM=%s: cannot open the file", e);
+}
+
+static void dev_open(void) {
+  int l, n;
+  if (D.n_dev) return;
+  sim_init();
+  if (D.want_n == 0) {
+    const char *e = getenv("FSCL_AMD_DEVICE");
+    if (!e) e = getenv("LOCAL_RANK");
+    D.want_dev[0] = e ? atoi(e) : 0;
+    n = 1;
+  } else if (D.want_n < 0) {
+    n = fsclg_device_count();
+    if (n > FH_MAX_DEV) n = FH_MAX_DEV;
+    for (l = 0; l < n; l++) D.want_dev[l] = l;
+  } else {
+    n = D.want_n;
+  }
+  if (n < 1) logmsg(MSG_FATAL, "fscl_amd: no GPU visible (%s); the scan path runs only on the GPU", fsclg_last_error());
+  for (l = 0; l < n; l++) {
+    const int r = fsclg_open(D.want_dev[l], &D.ctx[l]);
+    if (r != FSCLG_OK)
+      logmsg(MSG_FATAL, "fscl_amd: cannot open GPU %d (%s); the scan path runs only on the GPU", D.want_dev[l],
+             fsclg_last_error());
+    D.dev[l] = D.want_dev[l];
+    D.n_dev = l + 1;
+  }
+  if (n > 1) logmsg(MSG_STATUS, "fscl_amd: %d GPUs in this process", n);
+}
+
 static void free_rowmap(fh_rowmap_t *m) {
   free(m->depth_n); free(m->row_base); free(m->dev_row);
   memset(m, 0, sizeof *m);
 }
 
-/* flatten the sm_ptable_t spline trees into [row][interval][4] and upload */
-static void upload_tables(const sm_ptable_t *sm, int n_depths, const int *depth_n, const snp_t *snps,
-                          const int *idx, int n_idx) {
-  fh_rowmap_t *m = &D.rm;
+/* flatten the sm_ptable_t spline trees into [row][interval][4] and upload them to the
+   given contexts; device rows are those some site of snps (idx) uses, ranked by site count
+   (the device caches a window of every row in LDS), or every row when all_rows is set */
+static double *flatten_tables(fh_rowmap_t *m, const sm_ptable_t *sm, int n_depths, const int *depth_n,
+                              const snp_t *snps, const int *idx, int n_idx, int all_rows, double **nullrow_out,
+                              const double *null_known, int n_known) {
   int d, r, i;
   double *coef, *nullrow;
   unsigned char *seen;
@@ -170,12 +279,12 @@ static void upload_tables(const sm_ptable_t *sm, int n_depths, const int *depth_
     m->n_rows += depth_n[d] + 1 + depth_n[d] / 2 + 1;
   }
   m->n_iv = sm[0].spline_func[0]->n;
-  /* null_logl is a function of the row (scan-chromosome.c:23-37): take it from the sites;
-     the rows no site uses are dropped from the device tables */
+  /* null_logl is a function of the row (scan-chromosome.c:23-37): take it from the sites */
   seen = fh_calloc(m->n_rows, 1, "null rows");
   m->dev_row = fh_malloc(sizeof(int) * m->n_rows, "rowmap");
   {
     double *full_null = fh_calloc(m->n_rows, sizeof(double), "null rows");
+    if (null_known) memcpy(full_null, null_known, sizeof(double) * (size_t)(n_known < m->n_rows ? n_known : m->n_rows));
     for (i = 0; i < n_idx; i++) {
       const snp_t *p = snps + (idx ? idx[i] : i);
       const uint32_t rr = fh_full_row(m, p);
@@ -184,9 +293,11 @@ static void upload_tables(const sm_ptable_t *sm, int n_depths, const int *depth_
         logmsg(MSG_FATAL, "fscl_amd: null_logl differs between sites of the same class (call "
                           "compute_snp_null_model first)");
     }
-    /* device rows in descending order of site count (ties by row): the device caches a
-       prefix of them in LDS */
-    {
+    if (all_rows) {
+      for (r = 0; r < m->n_rows; r++) m->dev_row[r] = r;
+      m->n_dev_rows = m->n_rows;
+    } else {
+      /* device rows in descending order of site count (ties by row) */
       long long *cnt = fh_calloc(m->n_rows, sizeof(long long), "row counts");
       int *ord = fh_malloc(sizeof(int) * m->n_rows, "row order");
       int nu = 0, a, b;
@@ -206,7 +317,7 @@ static void upload_tables(const sm_ptable_t *sm, int n_depths, const int *depth_
     }
     if (m->n_dev_rows == 0) m->n_dev_rows = 1;  /* no sites: one zero row keeps the tables well-formed */
     nullrow = fh_calloc(m->n_dev_rows, sizeof(double), "null rows");
-    for (r = 0; r < m->n_rows; r++) if (seen[r]) nullrow[m->dev_row[r]] = full_null[r];
+    for (r = 0; r < m->n_rows; r++) if (m->dev_row[r] >= 0) nullrow[m->dev_row[r]] = full_null[r];
     free(full_null);
   }
   coef = fh_calloc((size_t)m->n_dev_rows * m->n_iv * 4, sizeof(double), "flat tables");
@@ -220,20 +331,24 @@ static void upload_tables(const sm_ptable_t *sm, int n_depths, const int *depth_
       for (i = 0; i < sp->n; i++) memcpy(coef + ((size_t)dr * m->n_iv + i) * 4, sp->coef[i], sizeof(double) * 4);
     }
   }
-  /* log_ad_step of the tables' knot grid (sm-spline.c:325) */
-  dev_check(fsclg_upload_tables(D.ctx, fh_log_table(), coef, m->n_dev_rows, m->n_iv, nullrow,
-                                (LOG_AD_MAX - LOG_AD_MIN) / (m->n_iv + 1.)),
-            "upload tables");
-  free(D.nullrow);
-  D.nullrow = nullrow;
-  free(coef);
   free(seen);
-  {
-    double coarse[16], refine[17 * 16];
-    int32_t nref[17];
-    const int nc = fh_alpha_grid(coarse, 16, refine, nref);
-    if (nc <= 0) logmsg(MSG_FATAL, "fscl_amd: alpha grid");
-    dev_check(fsclg_set_alpha_grid(D.ctx, coarse, nc, refine, nref), "alpha grid");
+  *nullrow_out = nullrow;
+  return coef;
+}
+
+static void upload_flat(fsclg_ctx *const *ctx, int n_ctx, const fh_rowmap_t *m, const double *coef,
+                        const double *nullrow) {
+  double coarse[16], refine[17 * 16];
+  int32_t nref[17];
+  const int nc = fh_alpha_grid(coarse, 16, refine, nref);
+  int l;
+  if (nc <= 0) logmsg(MSG_FATAL, "fscl_amd: alpha grid");
+  for (l = 0; l < n_ctx; l++) {
+    /* log_ad_step of the tables' knot grid (sm-spline.c:325) */
+    dev_check(fsclg_upload_tables(ctx[l], fh_log_table(), coef, m->n_dev_rows, m->n_iv, nullrow,
+                                  (LOG_AD_MAX - LOG_AD_MIN) / (m->n_iv + 1.)),
+              "upload tables");
+    dev_check(fsclg_set_alpha_grid(ctx[l], coarse, nc, refine, nref), "alpha grid");
   }
 }
 
@@ -243,36 +358,48 @@ static void check_site(const scan_t *s, const snp_t *p) {
     logmsg(MSG_FATAL, "fscl_amd: site class %d out of range for depth %d (folded=%d)", p->obs_freq, n, p->folded);
 }
 
-static uint64_t fnv1a(const void *p, size_t n, uint64_t h) {
+/* content hash (64-bit words, multiply-xorshift), for the device caches' keys */
+static uint64_t hash_words(const void *p, size_t n, uint64_t h) {
   const unsigned char *b = p;
   size_t i;
-  for (i = 0; i < n; i++) { h ^= b[i]; h *= 1099511628211ull; }
+  for (i = 0; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, b + i, 8);
+    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+  }
+  for (; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
   return h;
 }
 
-/* make the device hold this scan's sites and these tables; the cache key is a
-   hash of the content (a freed and re-allocated scan may reuse addresses) */
+/* make every local device hold this scan's sites and these tables; the cache key is a hash
+   of the content (a freed and re-allocated scan may reuse addresses) */
 static void prepare(scan_t *s, sm_ptable_t *sm) {
-  int i, d;
+  int i, d, l;
   uint64_t key = 1469598103934665603ull;
+  double *coef, *nullrow;
   init_log_table();
   dev_open();
-  key = fnv1a(&s->n_snps, sizeof s->n_snps, key);
-  key = fnv1a(s->snps, sizeof(snp_t) * (size_t)s->n_snps, key);
-  key = fnv1a(s->sample_depths, sizeof(int) * (size_t)s->n_depths, key);
-  for (i = 0; i < s->n_chromosomes; i++) key = fnv1a(&s->chr_limits[i].start_index, 4 * sizeof(int), key);
+  key = hash_words(&s->n_snps, sizeof s->n_snps, key);
+  key = hash_words(s->snps, sizeof(snp_t) * (size_t)s->n_snps, key);
+  key = hash_words(s->sample_depths, sizeof(int) * (size_t)s->n_depths, key);
+  for (i = 0; i < s->n_chromosomes; i++) key = hash_words(&s->chr_limits[i].start_index, 4 * sizeof(int), key);
   for (d = 0; d < s->n_depths; d++) {
     const int n = sm[d].sample_size;
-    key = fnv1a(&n, sizeof n, key);
+    key = hash_words(&n, sizeof n, key);
     for (i = 0; i <= n + n / 2 + 1; i++) {
       const spline_t *sp = i <= n ? sm[d].spline_func[i] : sm[d].fspline_func[i - n - 1];
-      key = fnv1a(sp->coef[0], sizeof(double) * 4 * (size_t)sp->n, key);
+      key = hash_words(sp->coef[0], sizeof(double) * 4 * (size_t)sp->n, key);
     }
   }
   if (D.snp_key && key == D.key) return;
-  DBG("prepare: uploading %d sites, %d depths\n", s->n_snps, s->n_depths);
+  DBG("prepare: uploading %d sites, %d depths to %d device(s)\n", s->n_snps, s->n_depths, D.n_dev);
   for (i = 0; i < s->n_snps; i++) check_site(s, s->snps + i);
-  upload_tables(sm, s->n_depths, s->sample_depths, s->snps, NULL, s->n_snps);
+  coef = flatten_tables(&D.rm, sm, s->n_depths, s->sample_depths, s->snps, NULL, s->n_snps, 0, &nullrow, NULL, 0);
+  upload_flat(D.ctx, D.n_dev, &D.rm, coef, nullrow);
+  free(coef);
+  free(D.nullrow);
+  D.nullrow = nullrow;
   free(D.row); free(D.pos); free(D.chr_start); free(D.chr_n);
   D.row = fh_malloc(sizeof(uint32_t) * s->n_snps, "rows");
   D.pos = fh_malloc(sizeof(int32_t) * s->n_snps, "positions");
@@ -287,7 +414,17 @@ static void prepare(scan_t *s, sm_ptable_t *sm) {
     D.chr_start[i] = s->chr_limits[i].start_index;
     D.chr_n[i] = s->chr_limits[i].n_snps;
   }
-  dev_check(fsclg_upload_snps(D.ctx, D.pos, D.row, s->n_snps, D.chr_start, D.chr_n, D.n_chr), "upload snps");
+  for (l = 0; l < D.n_dev; l++)
+    dev_check(fsclg_upload_snps(D.ctx[l], D.pos, D.row, s->n_snps, D.chr_start, D.chr_n, D.n_chr), "upload snps");
+  if (D.stage_cap < s->n_snps) {
+    int k;
+    for (k = 0; k < FSCLG_N_SLOTS; k++) {
+      fsclg_host_free(D.stage[k]);
+      D.stage[k] = fsclg_host_alloc(sizeof(uint32_t) * (size_t)s->n_snps);
+      if (!D.stage[k]) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
+    }
+    D.stage_cap = s->n_snps;
+  }
   D.tab_key = sm; D.snp_key = s->snps; D.n_snps_key = s->n_snps; D.key = key;
 }
 
@@ -303,8 +440,8 @@ static void chr_null_sums(const uint32_t *row, double *out) {
   }
 }
 
-/* contiguous share [lo, hi) of n items for one rank: item i belongs to the
-   rank whose slice of the total cost holds the cost accumulated before i */
+/* contiguous share [lo, hi) of n items for one share index: item i belongs to the
+   share whose slice of the total cost holds the cost accumulated before i */
 void fscl_amd_partition(const double *cost, int n, int rank, int world, int *lo, int *hi) {
   double tot = 0., acc = 0.;
   int i;
@@ -320,38 +457,71 @@ void fscl_amd_partition(const double *cost, int n, int rank, int world, int *lo,
   }
 }
 
-static void rank_share(const double *cost, int n, int *lo, int *hi) {
-  fscl_amd_partition(cost, n, D.rank, D.world, lo, hi);
+/* the local devices' shares of n items: lo[l], hi[l] (consecutive; this process's range is
+   [lo[0], hi[n_dev - 1])) */
+static void dev_shares(const double *cost, int n, int *lo, int *hi) {
+  const int T = D.world * D.n_dev;
+  int l;
+  for (l = 0; l < D.n_dev; l++) {
+    if (T <= 1) { lo[l] = 0; hi[l] = n; continue; }
+    fscl_amd_partition(cost, n, D.rank * D.n_dev + l, T, &lo[l], &hi[l]);
+  }
 }
 
-static void exchange(long long *buf, int n) {
-  if (D.world > 1 && n > 0)
-    if (D.xfn(buf, n, D.xctx) != 0) logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
+/* complete a batch's results on every rank: this process holds [lo, hi) of out[n] */
+static void exchange_points(fsclg_point_t *out, int n, int lo, int hi) {
+  if (D.sim) {
+    if (!D.sim_replay) {
+      if (fwrite(&n, sizeof n, 1, D.sim) != 1 || fwrite(out, sizeof(fsclg_point_t), (size_t)n, D.sim) != (size_t)n)
+        logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM record write failed");
+    } else {
+      fsclg_point_t *rec = fh_malloc(sizeof(fsclg_point_t) * (n ? n : 1), "sim");
+      int m = -1, i;
+      if (fread(&m, sizeof m, 1, D.sim) != 1 || m != n || fread(rec, sizeof(fsclg_point_t), (size_t)n, D.sim) != (size_t)n)
+        logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM replay: batch of %d cells, recording has %d", n, m);
+      for (i = lo; i < hi; i++)
+        if (memcmp(&rec[i].lalpha, &out[i].lalpha, 4 * sizeof(double)) != 0)
+          logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM replay: cell %d of a batch differs from the recording", i);
+      memcpy(out, rec, sizeof(fsclg_point_t) * (size_t)n);
+      free(rec);
+    }
+    return;
+  }
+  if (D.world <= 1 || n == 0) return;
+  if (D.shm) {
+    if (fh_shm_allgather(D.shm, out, sizeof(fsclg_point_t), n, lo, hi) != 0)
+      logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
+    return;
+  }
+  memset(out, 0, sizeof(fsclg_point_t) * (size_t)lo);
+  memset(out + hi, 0, sizeof(fsclg_point_t) * (size_t)(n - hi));
+  if (D.xfn((long long *)out, (int)(n * (sizeof(fsclg_point_t) / sizeof(long long))), D.xctx) != 0)
+    logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
 }
 
-/* evaluate cells on this rank's share, assemble all results on every rank */
+/* the cost of a cell: its window size (snp_likelihood terms scale with it) */
+static double window_cost(int chr, int eval_range) {
+  return (double)(D.chr_n[chr] < 2 * eval_range + 1 ? D.chr_n[chr] : 2 * eval_range + 1);
+}
+
+/* evaluate cells, each local device its share, then complete the results on every rank */
 static void eval_cells(const fsclg_cell_t *cells, int n, int eval_range, int bp_resl, fsclg_point_t *out) {
   double *cost = NULL;
-  int lo = 0, hi = n, i, r;
-  if (D.world > 1) {
+  int lo[FH_MAX_DEV], hi[FH_MAX_DEV], l, i;
+  if (D.world * D.n_dev > 1) {
     cost = fh_malloc(sizeof(double) * (n ? n : 1), "cost");
-    for (i = 0; i < n; i++) /* a cell's work scales with its window */
-      cost[i] = (double)(D.chr_n[cells[i].chr] < 2 * eval_range + 1 ? D.chr_n[cells[i].chr] : 2 * eval_range + 1);
-    rank_share(cost, n, &lo, &hi);
-    memset(out, 0, sizeof(fsclg_point_t) * n);
+    for (i = 0; i < n; i++) cost[i] = window_cost(cells[i].chr, eval_range);
   }
-  for (i = lo; i < hi; i += 1 << 16) {
-    const int m = hi - i < (1 << 16) ? hi - i : (1 << 16);
-    DBG("search_maxpos: %d cells from %d\n", m, i);
-    r = fsclg_search_maxpos(D.ctx, cells + i, m, eval_range, bp_resl, out + i);
-    DBG("search_maxpos: done (%d)\n", r);
-    dev_check(r, "search_maxpos");
+  dev_shares(cost, n, lo, hi);
+  free(cost);
+  for (l = 0; l < D.n_dev; l++) {
+    DBG("search_maxpos: device %d, cells [%d, %d)\n", D.dev[l], lo[l], hi[l]);
+    dev_check(fsclg_search_submit(D.ctx[l], 0, 0, cells + lo[l], hi[l] - lo[l], eval_range, bp_resl),
+              "search submit");
+    D.st.gp_evals += (unsigned long long)(hi[l] - lo[l]);
   }
-  D.st.gp_evals += (unsigned long long)(hi - lo);
-  if (D.world > 1) {
-    exchange((long long *)out, (int)(n * (sizeof(fsclg_point_t) / sizeof(long long))));
-    free(cost);
-  }
+  for (l = 0; l < D.n_dev; l++) dev_check(fsclg_search_wait(D.ctx[l], 0, out + lo[l]), "search wait");
+  exchange_points(out, n, lo[0], hi[D.n_dev - 1]);
 }
 
 static void to_scan_pt(scan_pt_t *p, const fsclg_point_t *o) {
@@ -369,14 +539,26 @@ static int pt_cmp(const void *va, const void *vb) {
   return a->seq - b->seq; /* scan-chromosome.c:218-225 under glibc's stable merge sort */
 }
 
+/* the unpermuted rows and whole-chromosome null sums into slot 0 of every device */
+static void set_original_rows(void) {
+  double *nul = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
+  int l;
+  chr_null_sums(D.row, nul);
+  for (l = 0; l < D.n_dev; l++) {
+    dev_check(fsclg_set_rows(D.ctx[l], NULL), "set rows");
+    dev_check(fsclg_set_chr_null(D.ctx[l], nul), "set null sums");
+  }
+  free(nul);
+}
+
 /* scan-chromosome.c:228-265 */
 void scan_chromosome(scan_t *s, sm_ptable_t *sm, int eval_range, int bp_resl, int large_grid_sp, int n_threads) {
   fsclg_cell_t *cells;
   fsclg_point_t *out;
   keyed_pt_t *kp;
   int n = 0, cap = 1024, chm = 0, pos, i;
-  double *nul, t0 = fh_now();
-  (void)n_threads; /* the GPU evaluates every cell concurrently */
+  double t0 = fh_now();
+  (void)n_threads; /* the GPUs evaluate every cell concurrently */
   prepare(s, sm);
   /* the cell sequence one scan_thread walks (scan-chromosome.c:176-212) */
   cells = fh_malloc(sizeof(fsclg_cell_t) * cap, "cells");
@@ -397,20 +579,22 @@ void scan_chromosome(scan_t *s, sm_ptable_t *sm, int eval_range, int bp_resl, in
       pos += large_grid_sp;
     }
   }
-  nul = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
-  chr_null_sums(D.row, nul);
-  dev_check(fsclg_set_rows(D.ctx, NULL), "set rows");
-  dev_check(fsclg_set_chr_null(D.ctx, nul), "set null sums");
+  set_original_rows();
   out = fh_malloc(sizeof(fsclg_point_t) * (n ? n : 1), "points");
   eval_cells(cells, n, eval_range, bp_resl, out);
   kp = fh_malloc(sizeof(keyed_pt_t) * (n ? n : 1), "points");
   for (i = 0; i < n; i++) { to_scan_pt(&kp[i].p, out + i); kp[i].seq = i; }
   qsort(kp, n, sizeof(keyed_pt_t), pt_cmp);
+  if (s->scan_pts)
+    for (i = 0; i < s->n_scan_pts; i++) free(s->scan_pts[i].permute_clr);
   free(s->scan_pts);
   s->scan_pts = fh_malloc(sizeof(scan_pt_t) * (n ? n : 1), "scan points");
-  for (i = 0; i < n; i++) s->scan_pts[i] = kp[i].p;
+  for (i = 0; i < n; i++) { /* scan-chromosome.c:239-241: a null-distribution buffer per point */
+    s->scan_pts[i] = kp[i].p;
+    s->scan_pts[i].permute_clr = fh_malloc(sizeof(float) * CLR_NULL_DIST_SAVE, "permute_clr");
+  }
   s->n_scan_pts = n;
-  free(kp); free(out); free(cells); free(nul);
+  free(kp); free(out); free(cells);
   D.st.scan_s += fh_now() - t0;
   logmsg(MSG_STATUS, "\nInitial scan finished.\n");
 }
@@ -472,9 +656,23 @@ static void block_permute(uint32_t *prow, const uint32_t *row, const snp_t *snps
   }
 }
 
+/* one trial's rows (in D.stage[slot]) and null sums to the slot on every local device;
+   waits until the slot's previous upload has read the staging before it is rewritten */
+static uint32_t *slot_stage(int slot) {
+  int l;
+  for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_wait(D.ctx[l], slot), "slot wait");
+  return D.stage[slot];
+}
+
+static void slot_upload(int slot, const double *nul) {
+  int l;
+  for (l = 0; l < D.n_dev; l++)
+    dev_check(fsclg_slot_set_rows_host(D.ctx[l], slot, D.stage[slot], nul), "set rows");
+}
+
 static volatile sig_atomic_t g_sigint = 0;
 static struct timeval g_last_dump;
-static void on_sigint(int sig) { /* scan-chromosome.c:557-569 */
+static void on_sigint(int sig) { /* scan-chromosome.c:553-560 */
   struct timeval now;
   (void)sig;
   gettimeofday(&now, NULL);
@@ -487,6 +685,20 @@ static void on_sigint(int sig) { /* scan-chromosome.c:557-569 */
 }
 
 static void output_clr_null_distribution(const char *fname, scan_t *s);
+
+/* scan-chromosome.c:553-560, taken between trials: the current table and null distributions
+   (one writer: rank 0); every rank restarts its 10-second window, so a second interrupt
+   ends all ranks alike */
+static void sigint_dump(scan_t *s, int n_perm) {
+  const char *fn = g_dump_set ? g_dump_fname : output_fname;
+  const char *lb = g_dump_set ? g_dump_label : prepend_label;
+  g_sigint = 0;
+  if (D.rank == 0) {
+    scan_output((char *)fn, s, 0, n_perm, (char *)lb);
+    if (fn) output_clr_null_distribution(fn, s);
+  }
+  gettimeofday(&g_last_dump, NULL);
+}
 
 /* ------------------------------------------------ pipelined permutation trials
    scan-chromosome.c:582-652 with --n-threads=1 pruning semantics, K trials in flight
@@ -526,11 +738,11 @@ typedef struct {
   fsclg_cell_t *cells;
   fsclg_point_t *out;
   int submitted;
-  int lo, hi;             /* this rank's share, fixed at submission */
+  int lo[FH_MAX_DEV], hi[FH_MAX_DEV];  /* the local devices' shares, fixed at submission */
 } trial_batch_t;
 
 /* per scan point: its permutation cell's cost in the last trial that evaluated it
-   (snp_likelihood terms / 1024, from the exchanged results, so identical on every rank);
+   (snp_likelihood terms / 1024, from the completed results, so identical on every rank);
    0 = not yet measured */
 static double *g_pcost;
 
@@ -544,45 +756,38 @@ static void tb_reserve(trial_batch_t *b, int n) {
 
 static void tb_free(trial_batch_t *b) { free(b->pt); free(b->cells); free(b->out); memset(b, 0, sizeof *b); }
 
-/* this rank's contiguous share of a batch by cost: a point's measured cell cost from its
-   last trial, else its window size (~32 terms / 1024 per window site) */
-static void tb_share(const trial_batch_t *b, int eval_range, int *lo, int *hi) {
-  double *cost;
-  int i;
-  *lo = 0; *hi = b->n;
-  if (D.world <= 1) return;
-  cost = fh_malloc(sizeof(double) * (b->n ? b->n : 1), "cost");
-  for (i = 0; i < b->n; i++) {
-    const int w = D.chr_n[b->cells[i].chr] < 2 * eval_range + 1 ? D.chr_n[b->cells[i].chr] : 2 * eval_range + 1;
-    cost[i] = g_pcost && g_pcost[b->pt[i]] > 0 ? g_pcost[b->pt[i]] : w / 32.0;
-  }
-  rank_share(cost, b->n, lo, hi);
-  free(cost);
-}
-
 static void tb_submit(trial_batch_t *b, int slot, int eval_range, int bp_resl) {
-  tb_share(b, eval_range, &b->lo, &b->hi);
-  if (D.world > 1) memset(b->out, 0, sizeof(fsclg_point_t) * b->n);
-  dev_check(fsclg_search_submit(D.ctx, b->batch, slot, b->cells + b->lo, b->hi - b->lo, eval_range, bp_resl),
-            "search submit");
+  double *cost = NULL;
+  int i, l;
+  if (D.world * D.n_dev > 1) {
+    /* a point's measured cell cost from its last trial, else its window size (~32 terms /
+       1024 per window site) */
+    cost = fh_malloc(sizeof(double) * (b->n ? b->n : 1), "cost");
+    for (i = 0; i < b->n; i++)
+      cost[i] = g_pcost && g_pcost[b->pt[i]] > 0 ? g_pcost[b->pt[i]] : window_cost(b->cells[i].chr, eval_range) / 32.0;
+  }
+  dev_shares(cost, b->n, b->lo, b->hi);
+  free(cost);
+  for (l = 0; l < D.n_dev; l++) {
+    dev_check(fsclg_search_submit(D.ctx[l], b->batch, slot, b->cells + b->lo[l], b->hi[l] - b->lo[l], eval_range,
+                                  bp_resl),
+              "search submit");
+    D.st.gp_evals += (unsigned long long)(b->hi[l] - b->lo[l]);
+  }
   b->submitted = 1;
-  D.st.gp_evals += (unsigned long long)(b->hi - b->lo);
 }
 
 /* wait for a batch and file each result in its point's queue */
-static void tb_wait(trial_batch_t *b, pqueue_t *pq, int eval_range) {
-  int k;
+static void tb_wait(trial_batch_t *b, pqueue_t *pq) {
+  int k, l;
   double tw = fh_now();
-  (void)eval_range;
   if (!b->submitted) return;
-  dev_check(fsclg_search_wait(D.ctx, b->batch, b->out + b->lo), "search wait");
+  for (l = 0; l < D.n_dev; l++) dev_check(fsclg_search_wait(D.ctx[l], b->batch, b->out + b->lo[l]), "search wait");
   b->submitted = 0;
   D.st.wait_s += fh_now() - tw;
-  if (D.world > 1) {
-    exchange((long long *)b->out, (int)(b->n * (sizeof(fsclg_point_t) / sizeof(long long))));
-    if (g_pcost)
-      for (k = 0; k < b->n; k++) g_pcost[b->pt[k]] = (double)b->out[k].cost;
-  }
+  exchange_points(b->out, b->n, b->lo[0], b->hi[D.n_dev - 1]);
+  if (g_pcost)
+    for (k = 0; k < b->n; k++) g_pcost[b->pt[k]] = (double)b->out[k].cost;
   for (k = 0; k < b->n; k++) {
     pqueue_t *q = pq + b->pt[k];
     int j;
@@ -636,7 +841,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   for (k = 0; k < K; k++) { Bt[k].batch = 2 + k; nul[k] = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums"); }
   act = fh_malloc(sizeof(int) * (n_act ? n_act : 1), "active points");
   pq = fh_calloc(n_act ? n_act : 1, sizeof(pqueue_t), "result queues");
-  if (D.world > 1) g_pcost = fh_calloc(n_act ? n_act : 1, sizeof(double), "point costs");
+  if (D.world * D.n_dev > 1) g_pcost = fh_calloc(n_act ? n_act : 1, sizeof(double), "point costs");
   tb_reserve(&A, n_act ? n_act : 1);
   for (k = 0; k < K; k++) tb_reserve(&Bt[k], n_act ? n_act : 1);
   for (i = 0; i < n_act; i++) act[i] = i;
@@ -647,13 +852,12 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     uint32_t *prow;
     /* the slot's previous trial: its bulk results (no draws among them) */
     if (B->submitted) {
-      tb_wait(B, pq, eval_range);
+      tb_wait(B, pq);
       for (k = 0; k < B->n; k++) pq_flush(s, pq, B->pt[k], done, -1, g, save);
     }
     D.st.search_s += fh_now() - tp;
     tp = fh_now();
-    prow = fsclg_slot_row_buffer(D.ctx, slot);
-    if (!prow) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
+    prow = slot_stage(slot);
     block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g);
     D.st.host_perm_s += fh_now() - tp;
     trial++;
@@ -666,7 +870,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     chr_null_sums(prow, nul[slot]);
     D.st.host_null_s += fh_now() - tp;
     tp = fh_now();
-    dev_check(fsclg_slot_set_rows(D.ctx, slot, prow, nul[slot]), "set rows");
+    slot_upload(slot, nul[slot]);
     D.st.host_upload_s += fh_now() - tp;
     tp = fh_now();
     A.n = B->n = 0;
@@ -687,11 +891,13 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       pq[a].n++;
     }
     D.st.n_crit += (unsigned long long)A.n;
-    if (A.n) tb_submit(&A, slot, eval_range, bp_resl);
-    if (B->n) tb_submit(B, slot, eval_range, bp_resl);
-    if (A.submitted) {
+    /* both batches always go through submit / wait (an empty share is a no-op), so that
+       every rank takes part in the same exchanges */
+    tb_submit(&A, slot, eval_range, bp_resl);
+    tb_submit(B, slot, eval_range, bp_resl);
+    {
       int drain = 0;
-      tb_wait(&A, pq, eval_range);
+      tb_wait(&A, pq);
       /* a point that may draw in this trial needs every earlier result applied first */
       for (k = 0; k < A.n && !drain; k++) {
         const int a = A.pt[k];
@@ -706,7 +912,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
           for (k = 0; k < K; k++)
             if (Bt[k].submitted && Bt[k].trial < trial && (!old || Bt[k].trial < old->trial)) old = &Bt[k];
           if (!old) break;
-          tb_wait(old, pq, eval_range);
+          tb_wait(old, pq);
           for (k = 0; k < old->n; k++) pq_flush(s, pq, old->pt[k], trial - 1, -1, g, save);
         }
       }
@@ -715,12 +921,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     done = trial;
     D.st.search_s += fh_now() - tp;
     D.st.trials++;
-    if (g_sigint && D.rank == 0) {
-      g_sigint = 0;
-      scan_output(output_fname, s, 0, n_permute, prepend_label);
-      if (output_fname) output_clr_null_distribution(output_fname, s);
-      gettimeofday(&g_last_dump, NULL);
-    }
+    if (g_sigint) sigint_dump(s, n_perm);
   }
   /* the bulk batches still in flight, oldest first */
   for (;;) {
@@ -729,7 +930,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     for (k = 0; k < K; k++)
       if (Bt[k].submitted && (!old || Bt[k].trial < old->trial)) old = &Bt[k];
     if (!old) break;
-    tb_wait(old, pq, eval_range);
+    tb_wait(old, pq);
     for (k = 0; k < old->n; k++) pq_flush(s, pq, old->pt[k], done, -1, g, save);
     D.st.search_s += fh_now() - tp;
   }
@@ -744,10 +945,10 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
 /* scan-chromosome.c:582-652 (with --n-threads=1 pruning semantics) */
 void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, double alpha_factor, int n_threads,
                   int eval_range, int bp_resl, int large_grid_sp, double scan_width_mb) {
-  fh_rand_t g;
+  fh_rand_t *g = perm_rng();
   uint32_t *prow;
   int *act, n_act = s->n_scan_pts, i, k, trial = -1;
-  const int save = n_perm + 1 < CLR_NULL_DIST_SAVE ? n_perm + 1 : CLR_NULL_DIST_SAVE;
+  const int save = CLR_NULL_DIST_SAVE; /* scan-chromosome.c:496 */
   fsclg_cell_t *cells;
   fsclg_point_t *out;
   double *nul, t0 = fh_now();
@@ -759,18 +960,14 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   sigemptyset(&sa.sa_mask);
   gettimeofday(&g_last_dump, NULL);
   sigaction(SIGINT, &sa, NULL);
-  fh_srand(&g, PERM_SEED);
-  (void)fh_rand(&g); /* scan-chromosome.c:440: the single thread's usleep() draw */
-  for (i = 0; i < s->n_scan_pts; i++)
-    if (!s->scan_pts[i].permute_clr) s->scan_pts[i].permute_clr = fh_malloc(sizeof(float) * (save > 0 ? save : 1), "permute_clr");
-  if (!getenv("FSCL_AMD_LOCKSTEP") && s->n_scan_pts <= (1 << 16)) {
-    permute_pipelined(s, n_perm, permute_nbp, eval_range, bp_resl, large_grid_sp, scan_width_mb, &g, save);
+  (void)fh_rand(g); /* scan-chromosome.c:440: the single thread's usleep() draw */
+  for (i = 0; i < s->n_scan_pts; i++) /* points a caller built without scan_chromosome */
+    if (!s->scan_pts[i].permute_clr) s->scan_pts[i].permute_clr = fh_malloc(sizeof(float) * save, "permute_clr");
+  if (!getenv("FSCL_AMD_LOCKSTEP")) {
+    permute_pipelined(s, n_perm, permute_nbp, eval_range, bp_resl, large_grid_sp, scan_width_mb, g, save);
     goto done;
   }
-  /* lockstep: permute -> rows to the device -> every active cell -> prune.  The permutation
-     is written straight into the device context's pinned staging */
-  prow = fsclg_row_buffer(D.ctx);
-  if (!prow) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
+  /* lockstep: permute -> rows to the devices -> every active cell -> prune */
   act = fh_malloc(sizeof(int) * (n_act ? n_act : 1), "active points");
   cells = fh_malloc(sizeof(fsclg_cell_t) * (n_act ? n_act : 1), "cells");
   out = fh_malloc(sizeof(fsclg_point_t) * (n_act ? n_act : 1), "points");
@@ -778,7 +975,8 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   for (i = 0; i < s->n_scan_pts; i++) act[i] = i;
   for (;;) {
     double tp = fh_now();
-    block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, &g);
+    prow = slot_stage(0);
+    block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g);
     D.st.host_perm_s += fh_now() - tp;
     trial++;
     for (i = k = 0; i < n_act; i++)
@@ -790,8 +988,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
     chr_null_sums(prow, nul);
     D.st.host_null_s += fh_now() - tp;
     tp = fh_now();
-    dev_check(fsclg_set_rows(D.ctx, prow), "set rows");
-    dev_check(fsclg_set_chr_null(D.ctx, nul), "set null sums");
+    slot_upload(0, nul);
     D.st.host_upload_s += fh_now() - tp;
     for (i = 0; i < n_act; i++) {
       const scan_pt_t *q = s->scan_pts + act[i];
@@ -810,7 +1007,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
       const double clr = out[i].clr;
       if (clr >= q->clr) {
         q->permute_p++;
-        if (q->permute_p >= 20 && q->permute_p / (double)q->permute_n >= fh_rand(&g) / (2147483647 + 1.0))
+        if (q->permute_p >= 20 && q->permute_p / (double)q->permute_n >= fh_rand(g) / (2147483647 + 1.0))
           q->permute_finished = 1; /* Q7: ratio uses the pre-increment count */
       }
       if (q->permute_n < save) q->permute_clr[q->permute_n] = (float)clr;
@@ -819,50 +1016,133 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
         fprintf(stderr, "%d\t%d\t%g\t%1.3e\n", q->chr, cells[i].start_pos, clr, exp(out[i].lalpha));
     }
     D.st.prune_s += fh_now() - tp;
-    if (g_sigint && D.rank == 0) {
-      g_sigint = 0;
-      scan_output(output_fname, s, 0, n_permute, prepend_label);
-      if (output_fname) output_clr_null_distribution(output_fname, s);
-      gettimeofday(&g_last_dump, NULL);
-    }
+    if (g_sigint) sigint_dump(s, n_perm);
   }
   free(act); free(cells); free(out); free(nul);
 done:
   cr_logmsg(MSG_STATUS, "Scanning snp block permutations... finished.\n");
   signal(SIGINT, SIG_DFL);
-  dev_check(fsclg_set_rows(D.ctx, NULL), "set rows");
+  set_original_rows();
   D.st.permute_s += fh_now() - t0;
 }
 
-/* sm-search.c:269-300 for one caller-initialised point (drop-in entry; the
-   scan path itself batches whole cells on the GPU) */
+/* --------------------------------------------------- search_maxalpha drop-in
+   sm-search.c:269-300 for one caller-initialised point.  The reference calls it once per
+   point from its own scan loop (scan-chromosome.c:126-135), so the drop-in keeps a context
+   of its own on the first device, with state that survives between calls:
+     * the tables, keyed by the sm_ptable_t pointer, the depths in use and a hash of the
+       coefficients (every row of those depths on the device; a row's null_logl, known only
+       from the sites, is added when a window first shows it);
+     * the sites of the last window uploaded, as (position, row) pairs: the next call reuses
+       them when its window lies inside and its sites compare equal (the caller's scan
+       loop evaluates many points of one window; a permuted array differs and is uploaded).
+   The scan path's own contexts are not touched. */
+static struct {
+  fsclg_ctx *ctx;
+  const sm_ptable_t *sm;
+  int n_depths;
+  uint64_t tab_hash;
+  fh_rowmap_t rm;
+  double *null_full;       /* [rm.n_rows] null_logl of each row, as seen so far */
+  unsigned char *null_seen;
+  int32_t *pos;            /* uploaded window [lo, lo + n) */
+  uint32_t *row;
+  int lo, n, cap;
+  int32_t *tpos;
+  uint32_t *trow;
+  int tcap;
+} DI;
+
+/* the first and last coefficient blocks of every row (tables are built once and never
+   changed by the reference; this catches a caller that rebuilds them in place) */
+static uint64_t tables_hash(const sm_ptable_t *sm, int n_depths) {
+  uint64_t h = 88172645463325252ull;
+  int d, i;
+  for (d = 0; d < n_depths; d++) {
+    const int n = sm[d].sample_size;
+    h = hash_words(&n, sizeof n, h);
+    for (i = 0; i <= n + n / 2 + 1; i++) {
+      const spline_t *sp = i <= n ? sm[d].spline_func[i] : sm[d].fspline_func[i - n - 1];
+      h = hash_words(sp->coef[0], sizeof(double) * 4, h);
+      h = hash_words(sp->coef[sp->n - 1], sizeof(double) * 4, h);
+    }
+  }
+  return h;
+}
+
+/* every row of depths [0, n_depths) on the drop-in context; the null values known so far
+   (rows of earlier depths keep their numbers when depths are added) plus this window's */
+static void dropin_tables(const sm_ptable_t *sm, int n_depths, const snp_t *snps, int ws, int n, int keep) {
+  int *dn = fh_malloc(sizeof(int) * n_depths, "depths"), *idx = fh_malloc(sizeof(int) * (n ? n : 1), "window");
+  const int n_known = keep ? DI.rm.n_rows : 0;
+  unsigned char *seen;
+  double *coef, *nullrow;
+  int d, i;
+  for (d = 0; d < n_depths; d++) dn[d] = sm[d].sample_size;
+  for (i = 0; i < n; i++) idx[i] = ws + i;
+  coef = flatten_tables(&DI.rm, sm, n_depths, dn, snps, idx, n, 1, &nullrow, DI.null_full, n_known);
+  seen = fh_calloc(DI.rm.n_rows, 1, "null rows");
+  if (n_known) memcpy(seen, DI.null_seen, (size_t)(n_known < DI.rm.n_rows ? n_known : DI.rm.n_rows));
+  for (i = 0; i < n; i++) seen[fh_full_row(&DI.rm, snps + ws + i)] = 1;
+  free(DI.null_full); free(DI.null_seen);
+  DI.null_full = nullrow;  /* every row: device row = row */
+  DI.null_seen = seen;
+  upload_flat(&DI.ctx, 1, &DI.rm, coef, nullrow);
+  free(coef); free(dn); free(idx);
+  DI.n = 0;  /* the tables were replaced: the sites go up again */
+}
+
 void search_maxalpha(scan_pt_t *pt, snp_t *snps, sm_ptable_t *sm) {
   const int ws = pt->window_start, we = pt->window_end, n = we - ws + 1;
-  int i, maxd = 0;
-  int *dn, *idx;
-  uint32_t *row;
-  int32_t *pos, cs, cn;
+  int i, maxd = 0, need_tables, reuse;
   fsclg_point_t p;
   init_log_table();
   dev_open();
+  if (!DI.ctx) dev_check(fsclg_open(D.dev[0], &DI.ctx), "open the search_maxalpha context");
+  if (n <= 0) logmsg(MSG_FATAL, "fscl_amd: search_maxalpha: empty window");
   for (i = ws; i <= we; i++) if (snps[i].depth_p > maxd) maxd = snps[i].depth_p;
-  dn = fh_malloc(sizeof(int) * (maxd + 1), "depths");
-  for (i = 0; i <= maxd; i++) dn[i] = sm[i].sample_size;
-  idx = fh_malloc(sizeof(int) * n, "window");
-  for (i = 0; i < n; i++) idx[i] = ws + i;
-  upload_tables(sm, maxd + 1, dn, snps, idx, n);
-  row = fh_malloc(sizeof(uint32_t) * n, "rows");
-  pos = fh_malloc(sizeof(int32_t) * n, "positions");
-  for (i = 0; i < n; i++) { row[i] = fh_row_of(&D.rm, snps + ws + i); pos[i] = snps[ws + i].pos; }
-  cs = 0; cn = n;
-  dev_check(fsclg_upload_snps(D.ctx, pos, row, n, &cs, &cn, 1), "upload window");
-  D.tab_key = NULL; D.snp_key = NULL; /* the device no longer holds a whole scan */
+  need_tables = DI.sm != sm || DI.n_depths < maxd + 1 || tables_hash(sm, DI.n_depths) != DI.tab_hash;
+  if (!need_tables) /* a row class this window shows for the first time: its null value */
+    for (i = ws; i <= we && !need_tables; i++) {
+      const uint32_t r = fh_full_row(&DI.rm, snps + i);
+      if (!DI.null_seen[r]) need_tables = 1;
+      else if (memcmp(&DI.null_full[r], &snps[i].null_logl, sizeof(double)) != 0)
+        logmsg(MSG_FATAL, "fscl_amd: null_logl differs between sites of the same class (call "
+                          "compute_snp_null_model first)");
+    }
+  if (need_tables) {
+    const int same = DI.sm == sm && DI.null_full != NULL;
+    const int nd = !same || maxd + 1 > DI.n_depths ? maxd + 1 : DI.n_depths;
+    dropin_tables(sm, nd, snps, ws, n, same);
+    DI.sm = sm; DI.n_depths = nd; DI.tab_hash = tables_hash(sm, nd);
+  }
+  /* the window's sites as the device holds them */
+  if (DI.tcap < n) {
+    DI.tcap = n;
+    DI.tpos = fh_realloc(DI.tpos, sizeof(int32_t) * n, "window");
+    DI.trow = fh_realloc(DI.trow, sizeof(uint32_t) * n, "window");
+  }
+  for (i = 0; i < n; i++) { DI.tpos[i] = snps[ws + i].pos; DI.trow[i] = fh_row_of(&DI.rm, snps + ws + i); }
+  reuse = DI.n > 0 && ws >= DI.lo && we < DI.lo + DI.n &&
+          !memcmp(DI.pos + (ws - DI.lo), DI.tpos, sizeof(int32_t) * n) &&
+          !memcmp(DI.row + (ws - DI.lo), DI.trow, sizeof(uint32_t) * n);
+  if (!reuse) {
+    int32_t cs = 0, cn = n;
+    if (DI.cap < n) {
+      DI.cap = n;
+      DI.pos = fh_realloc(DI.pos, sizeof(int32_t) * n, "window");
+      DI.row = fh_realloc(DI.row, sizeof(uint32_t) * n, "window");
+    }
+    memcpy(DI.pos, DI.tpos, sizeof(int32_t) * n);
+    memcpy(DI.row, DI.trow, sizeof(uint32_t) * n);
+    DI.lo = ws; DI.n = n;
+    dev_check(fsclg_upload_snps(DI.ctx, DI.pos, DI.row, n, &cs, &cn, 1), "upload window");
+  }
   memset(&p, 0, sizeof p);
-  p.chr = pt->chr; p.nearest_snp = pt->nearest_snp - ws; p.sweep_pos = pt->sweep_pos; p.n_snps = pt->n_snps;
-  p.window_start = 0; p.window_end = n - 1; p.null_logl = pt->null_logl;
-  dev_check(fsclg_search_points(D.ctx, &p, 1), "search_maxalpha");
+  p.chr = 0; p.nearest_snp = pt->nearest_snp - DI.lo; p.sweep_pos = pt->sweep_pos; p.n_snps = pt->n_snps;
+  p.window_start = ws - DI.lo; p.window_end = we - DI.lo; p.null_logl = pt->null_logl;
+  dev_check(fsclg_search_points(DI.ctx, &p, 1), "search_maxalpha");
   pt->lalpha = p.lalpha; pt->sm_logl = p.sm_logl; pt->clr = p.clr;
-  free(dn); free(idx); free(row); free(pos);
 }
 
 /* ---------------------------------------------------------------- output */
@@ -943,31 +1223,45 @@ static void output_clr_null_distribution(const char *fname, scan_t *s) {
 }
 
 /* ----------------------------------------------------------------- stats */
+/* this process's counters; device counters summed over its devices (busy_ms: the sum of
+   each device's busy time, i.e. device-seconds) */
 void fscl_amd_get_stats(fscl_amd_stats_t *st) {
+  int l;
   *st = D.st;
-  if (D.ctx) {
+  st->kernel_ms = 0; st->n_terms = st->n_null = st->n_walks = st->n_maxalpha = 0;
+  st->n_unsafe = st->n_slow = st->n_ties = st->n_launches = 0;
+  st->window_ms = 0; st->n_dup_cells = st->n_ep_saved = 0; st->busy_ms = 0;
+  for (l = 0; l < D.n_dev; l++) {
     fsclg_stats_t g;
-    if (fsclg_get_stats(D.ctx, &g) == FSCLG_OK) {
-      st->kernel_ms = g.kernel_ms;
-      st->n_terms = g.n_terms; st->n_null = g.n_null; st->n_walks = g.n_walks; st->n_maxalpha = g.n_maxalpha;
-      st->n_unsafe = g.n_unsafe; st->n_slow = g.n_slow; st->n_ties = g.n_ties; st->n_launches = g.n_launches;
+    if (fsclg_get_stats(D.ctx[l], &g) != FSCLG_OK) continue;
+    st->kernel_ms += g.kernel_ms;
+    st->n_terms += g.n_terms; st->n_null += g.n_null; st->n_walks += g.n_walks; st->n_maxalpha += g.n_maxalpha;
+    st->n_unsafe += g.n_unsafe; st->n_slow += g.n_slow; st->n_ties += g.n_ties; st->n_launches += g.n_launches;
+    st->window_ms += g.window_ms;
+    st->n_dup_cells += g.n_dup_cells; st->n_ep_saved += g.n_ep_saved;
+    st->busy_ms += g.busy_ms;
+    if (l == 0) {
       st->cache_iv0 = g.cache_iv0; st->cache_n_iv = g.cache_n_iv; st->cache_n_rows = g.cache_n_rows;
-      st->cache_cover = g.cache_cover; st->window_ms = g.window_ms;
-      st->n_dup_cells = g.n_dup_cells; st->n_ep_saved = g.n_ep_saved;
-      st->busy_ms = g.busy_ms;
+      st->cache_cover = g.cache_cover;
     }
   }
+  st->n_devices = D.n_dev;
 }
 
 void fscl_amd_reset_stats(void) {
+  int l;
   memset(&D.st, 0, sizeof D.st);
-  if (D.ctx) fsclg_reset_stats(D.ctx);
+  for (l = 0; l < D.n_dev; l++) fsclg_reset_stats(D.ctx[l]);
 }
 
 void fscl_amd_shutdown(void) {
-  if (D.ctx) fsclg_close(D.ctx);
-  D.ctx = NULL; D.tab_key = NULL; D.snp_key = NULL;
+  dev_close_all();
+  if (DI.ctx) fsclg_close(DI.ctx);
+  free(DI.null_full); free(DI.null_seen); free(DI.pos); free(DI.row); free(DI.tpos); free(DI.trow);
+  free_rowmap(&DI.rm);
+  memset(&DI, 0, sizeof DI);
   free(D.row); free(D.pos); free(D.chr_start); free(D.chr_n); free(D.nullrow);
   D.row = NULL; D.pos = NULL; D.chr_start = NULL; D.chr_n = NULL; D.nullrow = NULL;
   free_rowmap(&D.rm);
+  if (D.sim) { fclose(D.sim); D.sim = NULL; }
 }

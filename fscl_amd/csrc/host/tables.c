@@ -17,7 +17,7 @@
 
 #include "fscl_host.h"
 
-__attribute__((weak)) int spline_pts = N_SPLINE_KNOTS; /* fscl.c:179 defines it when linked */
+__attribute__((weak)) int spline_pts = N_SPLINE_KNOTS; /* fscl.c:34 defines it when linked */
 double log_ad_step = 24.0 / 201.0;                      /* sm-spline.c:16 */
 
 double fh_log_ad_step(void) { return log_ad_step; }

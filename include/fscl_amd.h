@@ -103,7 +103,7 @@ typedef struct {
 
 enum { MSG_FATAL = 0, MSG_ERROR, MSG_WARN, MSG_STATUS, MSG_DEBUG1, MSG_DEBUG2 };
 
-/* Globals the reference's fscl.c defines (fscl.c:178-179).  The library holds
+/* Globals the reference's fscl.c defines (fscl.c:33-34).  The library holds
    weak defaults so it also works without fscl.c; fscl.c's definitions win. */
 extern int spline_pts;
 extern int n_permute;
@@ -141,8 +141,23 @@ void cr_logmsg(int priority, volatile char *s, ...);
 scan_t *fscl_amd_load_ms_input(const char *ms_fname, int segment_length, int ms_folded, int sample_first,
                                int sample_size);
 
-/* device selection (default: $FSCL_AMD_DEVICE, else LOCAL_RANK, else 0) */
+/* the permutation rand() stream is process-wide and seeded once, as srand(0xFD821A6)
+   in the reference's init_options (fscl.c:135): it continues across scan_permute calls.
+   fscl_amd_srand restarts it (what a fresh process would see). */
+void fscl_amd_srand(unsigned seed);
+
+/* what a SIGINT during scan_permute writes (scan-chromosome.c:553-560): by default
+   fscl.c's globals output_fname / prepend_label; a library caller sets them here */
+void fscl_amd_set_dump_output(const char *fname, const char *label);
+
+/* device selection.  Default: one device, $FSCL_AMD_DEVICE, else LOCAL_RANK, else 0.
+   fscl_amd_set_devices(ids, n): this process drives n GPUs (ids NULL: 0 .. n-1; n = 0:
+   every visible GPU) -- each batch of grid cells is split into cost-balanced contiguous
+   shares, one per device, the host logic (permutation, pruning) runs once; results are
+   identical to one device.  fscl_amd_n_devices: the devices opened (0 before the first scan). */
 int fscl_amd_set_device(int device);
+int fscl_amd_set_devices(const int *devices, int n);
+int fscl_amd_n_devices(void);
 
 /* Multi-process parity mode (one process per GPU).  Every rank runs the same
    host logic (rand() stream, block permutation, pruning) and evaluates a
@@ -152,6 +167,14 @@ int fscl_amd_set_device(int device);
    exactly).  fn == NULL or world == 1: single process. */
 typedef int (*fscl_amd_exchange_fn)(long long *buf, int n, void *ctx);
 int fscl_amd_set_ranks(int rank, int world, fscl_amd_exchange_fn fn, void *ctx);
+
+/* The same with the library's own exchange: the ranks share one node, and each batch's
+   results are all-gathered through a POSIX shared-memory segment `name` (unique to the job,
+   e.g. "/fscl_amd_<uuid>"; created by rank 0, unlinked once every rank has attached).
+   Every rank calls it before its first scan; returns 0, or -1 if the ranks could not meet
+   (within $FSCL_AMD_RANK_TIMEOUT seconds, default 600).  $FSCL_AMD_SHM_MB (default 64)
+   bounds one exchange (64 B per grid cell of a batch). */
+int fscl_amd_set_ranks_shm(int rank, int world, const char *name);
 
 /* the cost-balanced contiguous split the ranks use: items [lo, hi) of n go to
    `rank` (costs: SNPs of the cell's chromosome, i.e. its window size) */
@@ -178,6 +201,7 @@ typedef struct {
   double wait_s;          /* scan_permute: host time blocked on trial results */
   unsigned long long n_crit;  /* scan_permute: cells in the trials' blocking (near-critical) batches */
   unsigned long long n_drain; /* scan_permute: trials that had to wait for every bulk batch in flight */
+  int n_devices;          /* local GPUs this process drives */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

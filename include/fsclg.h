@@ -26,6 +26,7 @@
 #ifndef FSCLG_H
 #define FSCLG_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -121,6 +122,17 @@ int fsclg_slot_set_rows(fsclg_ctx *c, int slot, const uint32_t *row, const doubl
 int fsclg_search_submit(fsclg_ctx *c, int batch, int slot, const fsclg_cell_t *cells, int n_cells, int eval_range,
                         int bp_resl);
 int fsclg_search_wait(fsclg_ctx *c, int batch, fsclg_point_t *out);
+
+/* Several devices fed from one host buffer.  fsclg_host_alloc returns pinned host memory that
+   every device's kernels read directly (portable, mapped, coherent); fsclg_slot_set_rows_host
+   uploads a slot's rows straight from such a buffer (no copy into the context's own staging,
+   no range check: every row must be < the n_rows of fsclg_upload_tables) and returns at once;
+   the caller keeps the buffer unchanged until fsclg_slot_wait(c, slot) has returned on every
+   context it was handed to (the slot's last upload has read it). */
+void *fsclg_host_alloc(size_t bytes);
+void fsclg_host_free(void *p);
+int fsclg_slot_wait(fsclg_ctx *c, int slot);
+int fsclg_slot_set_rows_host(fsclg_ctx *c, int slot, const uint32_t *row, const double *chr_null);
 
 /* sequential window null sums (init_scan_result's sum from 0.0) for each chromosome's
    whole-chromosome window, for the rows currently set */

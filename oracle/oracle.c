@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -711,6 +712,39 @@ void orc_scan_chromosome(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t
   if (st) stats_add(st, &tot);
 }
 
+/* CPU-baseline sample (bench.py): n_sample scan cells spread evenly over the genome
+   (every k-th cell of scan_chromosome's sequence; aligned: the G-aligned, unclipped cell
+   a permutation trial evaluates for the same point, scan-chromosome.c:481-486) evaluated on
+   snps with o->n_threads threads; returns the wall seconds and the cells evaluated */
+double orc_sample_cells(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t *o, const orc_snp_t *snps,
+                        int n_sample, int aligned, int *n_done) {
+  int n, i, m = 0;
+  cell_t *c = scan_cells(s, o->large_grid_sp, &n);
+  int *pick = xmalloc(sizeof(int) * (n_sample > 0 ? n_sample : 1));
+  struct timespec t0, t1;
+  for (i = 0; i < n_sample && n > 0; i++) {
+    const int k = (int)(((long long)i * n) / n_sample);
+    if (m == 0 || pick[m - 1] != k) pick[m++] = k;
+  }
+  if (aligned)
+    for (i = 0; i < m; i++) {
+      cell_t *x = c + pick[i];
+      x->start -= x->start % o->large_grid_sp;
+      x->end = x->start + o->large_grid_sp;
+    }
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(o->n_threads > 0 ? o->n_threads : 1)
+  for (i = 0; i < m; i++) {
+    const cell_t *x = c + pick[i];
+    orc_stats_t loc = {0};
+    (void)orc_search_maxpos(x->chr, x->start, x->end, snps, s->chr + x->chr, o->eval_range, o->bp_resl, tab, &loc);
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  free(pick); free(c);
+  if (n_done) *n_done = m;
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
 /* scan-chromosome.c:336-389, with Q9 (negative j) repaired as j -= k - n */
 void orc_block_permute(orc_snp_t *p, const orc_snp_t *snps, int n, double nbp, double width_mb,
                        orc_rand_t *g, orc_stats_t *st) {
@@ -744,21 +778,27 @@ void orc_block_permute(orc_snp_t *p, const orc_snp_t *snps, int n, double nbp, d
 /* scan-chromosome.c:391-652 with --n-threads=1 semantics: lockstep trials,
    points evaluated (in parallel if n_threads > 1), then the prune pass in
    ascending point order so the rand() stream is exactly the 1-thread one. */
+/* the rand() stream, seeded once per process as srand() in init_options (fscl.c:135): it
+   continues across orc_scan_permute calls; orc_reseed restarts it */
+static orc_rand_t g_rng;
+static int g_rng_seeded = 0;
+void orc_reseed(unsigned seed) { orc_srand(&g_rng, seed); g_rng_seeded = 1; }
+
 void orc_scan_permute(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t *o, orc_stats_t *st) {
-  orc_rand_t g;
+  orc_rand_t *const gp = &g_rng;
   orc_snp_t *ps = xmalloc(sizeof(orc_snp_t) * s->n_snps);
   int *act = xmalloc(sizeof(int) * (s->n_pts ? s->n_pts : 1)), n_act = s->n_pts, i, k, trial = -1;
   double *clr = xmalloc(sizeof(double) * (s->n_pts ? s->n_pts : 1));
-  int save = o->n_permute + 1 < CLR_NULL_DIST_SAVE ? o->n_permute + 1 : CLR_NULL_DIST_SAVE;
+  const int save = CLR_NULL_DIST_SAVE; /* scan-chromosome.c:240,496 */
   orc_stats_t tot = {0};
-  orc_srand(&g, 0xFD821A6); /* fscl.c:280 */
-  (void)orc_rand(&g);       /* scan-chromosome.c:440: the usleep() draw of the one thread */
+  if (!g_rng_seeded) orc_reseed(0xFD821A6);
+  (void)orc_rand(gp);       /* scan-chromosome.c:440: the usleep() draw of the one thread */
   for (i = 0; i < s->n_pts; i++) {
     act[i] = i;
-    s->pts[i].permute_clr = xmalloc(sizeof(float) * (save > 0 ? save : 1));
+    if (!s->pts[i].permute_clr) s->pts[i].permute_clr = xmalloc(sizeof(float) * CLR_NULL_DIST_SAVE);
   }
   for (;;) {
-    orc_block_permute(ps, s->snps, s->n_snps, o->permute_nbp, o->scan_width_mb, &g, &tot);
+    orc_block_permute(ps, s->snps, s->n_snps, o->permute_nbp, o->scan_width_mb, gp, &tot);
     trial++;
     for (i = k = 0; i < n_act; i++)
       if (!s->pts[act[i]].permute_finished) act[k++] = act[i];
@@ -782,7 +822,7 @@ void orc_scan_permute(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t *o
       orc_pt_t *q = s->pts + act[i];
       if (clr[i] >= q->clr) {
         q->permute_p++;
-        if (q->permute_p >= 20 && q->permute_p / (double)q->permute_n >= orc_rand(&g) / (2147483647 + 1.0))
+        if (q->permute_p >= 20 && q->permute_p / (double)q->permute_n >= orc_rand(gp) / (2147483647 + 1.0))
           q->permute_finished = 1; /* Q7 */
       }
       if (q->permute_n < save) q->permute_clr[q->permute_n] = (float)clr[i];
@@ -833,14 +873,14 @@ int orc_scan_output(const char *fname, orc_scan_t *s, int max_only, int n_permut
 
 void orc_default_opts(orc_opts_t *o) {
   memset(o, 0, sizeof(*o));
-  o->spline_pts = 200;      /* fscl.c:312 */
-  o->minimum_depth = 5;     /* fscl.c:294 */
-  o->asc_min_freq = 1;      /* fscl.c:290 */
-  o->permute_nbp = 0.1;     /* fscl.c:292 */
-  o->scan_width_mb = 1.0;   /* fscl.c:305 */
-  o->large_grid_sp = 100000;/* fscl.c:304 */
-  o->eval_range = 81920;    /* fscl.c:320 */
-  o->bp_resl = 128;         /* fscl.c:319 */
+  o->spline_pts = 200;      /* fscl.c:167 */
+  o->minimum_depth = 5;     /* fscl.c:149, :188 */
+  o->asc_min_freq = 1;      /* fscl.c:145 */
+  o->permute_nbp = 0.1;     /* fscl.c:147 */
+  o->scan_width_mb = 1.0;   /* fscl.c:160 */
+  o->large_grid_sp = 100000;/* fscl.c:159 */
+  o->eval_range = 81920;    /* fscl.c:175 */
+  o->bp_resl = 128;         /* fscl.c:174 */
   o->n_threads = 1;
 }
 
@@ -862,7 +902,7 @@ void orc_free_scan(orc_scan_t *s) {
   free(s->pts); free(s->chr); free(s->snps); free(s->sample_depths); free(s);
 }
 
-/* fscl.c:460-482 */
+/* fscl.c:316-337 */
 int orc_run_snpfile(const char *snp_fname, const char *out_fname, const orc_opts_t *o,
                     const char *label, orc_stats_t *st) {
   orc_scan_t *s;
@@ -870,6 +910,7 @@ int orc_run_snpfile(const char *snp_fname, const char *out_fname, const orc_opts
   orc_table_t *tab;
   int i;
   orc_init_log_table();
+  orc_reseed(0xFD821A6); /* init_options, fscl.c:135: a fresh process */
   s = orc_load_snp_input(snp_fname, o->include_invariant, o->minimum_depth);
   if (!s) return -1;
   fsp = orc_background_fsp(s, o->force_neutral, o->include_invariant);

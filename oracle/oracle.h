@@ -87,7 +87,7 @@ typedef struct {
 } orc_table_t;
 
 typedef struct {
-  int spline_pts;       /* --splines (fscl.c:229, default N_SPLINE_KNOTS) */
+  int spline_pts;       /* --splines (fscl.c:84, default N_SPLINE_KNOTS at :167) */
   int include_invariant;
   int minimum_depth;
   int force_neutral;
@@ -96,8 +96,8 @@ typedef struct {
   double permute_nbp;
   double scan_width_mb;
   int large_grid_sp;
-  int eval_range;       /* fscl.c:320 */
-  int bp_resl;          /* fscl.c:319 */
+  int eval_range;       /* fscl.c:175 */
+  int bp_resl;          /* fscl.c:174 */
   int max_only;
   int n_threads;        /* OpenMP threads for the lockstep-parallel port (results identical) */
 } orc_opts_t;
@@ -116,6 +116,8 @@ typedef struct {
 typedef struct { int32_t r[31]; int f, b; } orc_rand_t;
 void orc_srand(orc_rand_t *g, unsigned seed);
 int orc_rand(orc_rand_t *g);
+/* restart the process-wide permutation stream (srand, fscl.c:135) */
+void orc_reseed(unsigned seed);
 
 void orc_default_opts(orc_opts_t *o);
 void orc_init_log_table(void);
@@ -144,9 +146,13 @@ void orc_scan_chromosome(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t
 void orc_block_permute(orc_snp_t *p, const orc_snp_t *snps, int n, double nbp, double width_mb,
                        orc_rand_t *g, orc_stats_t *st);
 void orc_scan_permute(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t *o, orc_stats_t *st);
+/* CPU-baseline sample: n_sample evenly spread scan cells (aligned: their permutation-trial
+   cells) evaluated on snps; returns wall seconds, *n_done the cells evaluated */
+double orc_sample_cells(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t *o, const orc_snp_t *snps,
+                        int n_sample, int aligned, int *n_done);
 int orc_scan_output(const char *fname, orc_scan_t *s, int max_only, int n_permute, const char *label);
 
-/* whole CLI pipeline on a SNP file (fscl.c:460-482); returns 0 on success */
+/* whole CLI pipeline on a SNP file (fscl.c:316-337); returns 0 on success */
 int orc_run_snpfile(const char *snp_fname, const char *out_fname, const orc_opts_t *o,
                     const char *label, orc_stats_t *st);
 

@@ -49,6 +49,7 @@ def load() -> C.CDLL:
     L.orc_null_model.argtypes = [P(OrcScan), C.c_void_p]
     L.orc_scan_chromosome.argtypes = [P(OrcScan), C.c_void_p, P(OrcOpts), P(OrcStats)]
     L.orc_scan_permute.argtypes = [P(OrcScan), C.c_void_p, P(OrcOpts), P(OrcStats)]
+    L.orc_reseed.argtypes = [C.c_uint]
     return L
 
 
@@ -71,6 +72,25 @@ class OracleScan:
 
     def scan(self) -> None:
         self.L.orc_scan_chromosome(self.s, self.tab, C.byref(self.o), C.byref(self.stats))
+
+    def reseed(self, seed: int = 0xFD821A6) -> None:
+        """Restart the oracle's process-wide permutation stream (srand, fscl.c:135)."""
+        self.L.orc_reseed(seed)
+
+    def permute(self, n_permute: int) -> None:
+        """One scan_permute call (the stream continues from the previous call)."""
+        self.o.n_permute = n_permute
+        self.L.orc_scan_permute(self.s, self.tab, C.byref(self.o), C.byref(self.stats))
+
+    def points(self) -> list[tuple]:
+        """(chr, sweep_pos, clr, lalpha, sm_logl, null_logl, nearest, ws, we, permute_n, permute_p, finished)"""
+        s = self.s.contents
+        out = []
+        for i in range(s.n_pts):
+            q = s.pts[i]
+            out.append((q.chr, q.sweep_pos, q.clr, q.lalpha, q.sm_logl, q.null_logl, q.nearest_snp, q.window_start,
+                        q.window_end, q.permute_n, q.permute_p, q.permute_finished))
+        return out
 
     def clr(self) -> list[tuple[int, int, float]]:
         s = self.s.contents

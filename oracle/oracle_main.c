@@ -1,9 +1,9 @@
 /*
  * oracle_main.c -- command line front end of the CPU restatement (test
- * infrastructure only).  Mirrors fscl's option table (fscl.c:183-247),
- * defaults (fscl.c:272-323), validation (fscl.c:325-403) and the
+ * infrastructure only).  Mirrors fscl's option table (fscl.c:38-102),
+ * defaults (fscl.c:127-178), validation (fscl.c:180-258) and the
  * "--long=value" / "-x value" parsing of cmdline-utils.c:28-100.
- * Supports the SNP-file path (fscl.c:460-482); -m (ms input) is routed by
+ * Supports the SNP-file path (fscl.c:316-337); -m (ms input) is routed by
  * the product CLI's converter, see DESIGN.md.
  */
 #include <stdio.h>

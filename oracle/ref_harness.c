@@ -8,6 +8,9 @@
  *   ref_harness tables <snpfile> <out.bin> [opts]
  *       load_snp_input -> background_fsp -> compute_sweep_model_tables
  *       (all reference code) and dump fsp + every spline coefficient.
+ *   ref_harness sample <snpfile> <n_cells> [opts]
+ *       the CPU baseline's bounded sample (bench.py): n_cells evenly spread scan cells,
+ *       one block permutation, and those cells' permutation-trial cells, timed.
  *   ref_harness scan <snpfile> <out.txt> <dump.txt> [opts]
  *       reference setup + the reference's search_maxalpha (sm-search.c:269)
  *       plugged into oracle.c's restatement of scan-chromosome.c (which cannot
@@ -30,7 +33,7 @@
 #include "fscl.h" /* the reference's own header, from -I/root/reference */
 #include "oracle.h"
 
-int spline_pts = N_SPLINE_KNOTS; /* defined in fscl.c:179, which cannot be built here */
+int spline_pts = N_SPLINE_KNOTS; /* defined in fscl.c:34, which cannot be built here */
 
 _Static_assert(sizeof(snp_t) == sizeof(orc_snp_t), "snp_t layout");
 _Static_assert(offsetof(snp_t, null_logl) == offsetof(orc_snp_t, null_logl), "snp_t layout");
@@ -117,6 +120,31 @@ int main(int argc, char **argv) {
     orc_dump_points(argv[4], os);
     fprintf(stderr, "ref_harness: gp=%lld maxalpha=%lld negj=%lld\n", st.n_gp, st.n_maxalpha, st.negj);
     return st.negj ? 3 : 0;
+  }
+  if (!strcmp(argv[1], "sample")) {
+    /* ref_harness sample <snpfile> <n_cells> [opts]: the CPU baseline's bounded sample --
+       n_cells evenly spread scan cells through the reference's own search_maxalpha (with
+       --n-threads threads), then one block permutation (serial, as in the reference:
+       scan-chromosome.c:441-456) and the same cells' permutation-trial cells on it */
+    orc_scan_t *os = (orc_scan_t *)s;
+    orc_snp_t *ps = malloc(sizeof(orc_snp_t) * (size_t)os->n_snps);
+    orc_rand_t g;
+    struct timespec t0, t1;
+    int ns = atoi(argv[3]), done = 0, pdone = 0, r, reps = 3;
+    double cell_s, pcell_s, perm_s;
+    orc_null_model(os, fsp);
+    orc_set_maxalpha_hook(ref_maxalpha, sm);
+    cell_s = orc_sample_cells(os, NULL, &o, os->snps, ns, 0, &done);
+    orc_srand(&g, 0xFD821A6);
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (r = 0; r < reps; r++) orc_block_permute(ps, os->snps, os->n_snps, o.permute_nbp, o.scan_width_mb, &g, &st);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    perm_s = ((double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec)) / reps;
+    pcell_s = orc_sample_cells(os, NULL, &o, ps, ns, 1, &pdone);
+    fprintf(stderr, "ref_harness: sample_cells=%d threads=%d cell_s=%.6f perm_gen_s=%.6f perm_cells=%d perm_cell_s=%.6f\n",
+            done, o.n_threads, cell_s, perm_s, pdone, pcell_s);
+    free(ps);
+    return 0;
   }
   fprintf(stderr, "ref_harness: unknown mode %s\n", argv[1]);
   return 2;

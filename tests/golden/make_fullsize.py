@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Expected results of the full-size BASELINE workloads that are too slow to run
+the oracle live on the GPU box (test infrastructure).
+
+For each case: regenerate the seeded synthetic input (fscl_amd/synth.py), run the
+oracle (oracle/_build/fscl_oracle, the CPU restatement pinned by the golden
+fixtures of make_golden.py) and store, in fullsize.json,
+  * the SHA-256 of the input file (the box regenerates it and checks the digest),
+  * the SHA-256 of the canonical scan-point dump (every field of every point, floats as
+    C99 hex: canonical_dump() below) and of the output file,
+  * every 97th dump row for diagnostics.
+
+    python tests/golden/make_fullsize.py [case ...] [--threads N]
+
+Cases (SURVEY §8(d) / BASELINE.json):
+  C5_full     22 x 227k SNPs (5.0M), n=400, initial scan          (configs[4] genome)
+  C5_chr_p200 one C5 chromosome, --n-permute=200 (early prune)    (configs[4] regime)
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+from fscl_amd import synth  # noqa: E402
+from util import ORACLE, read_dump  # noqa: E402
+
+CASES = {
+    "C5_full": dict(gen=dict(n_chr=22, chr_len=227_272_727, snps_per_chr=227_273, n=400, seed=55, sweeps_per_chr=2),
+                    opts=[]),
+    "C5_chr_p200": dict(gen=dict(n_chr=1, chr_len=227_272_727, snps_per_chr=227_273, n=400, seed=57,
+                                 sweeps_per_chr=2), opts=["--n-permute=200"]),
+}
+
+
+def sha256_file(p: Path) -> str:
+    h = hashlib.sha256()
+    with open(p, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
+def canonical_row(r: tuple) -> str:
+    return "\t".join(x.hex() if isinstance(x, float) else str(x) for x in r)
+
+
+def canonical_dump(rows: list[tuple]) -> str:
+    h = hashlib.sha256()
+    for r in rows:
+        h.update(canonical_row(r).encode())
+        h.update(b"\n")
+    return h.hexdigest()
+
+
+def main(argv: list[str]) -> int:
+    threads = os.cpu_count() or 1
+    names = []
+    it = iter(argv)
+    for a in it:
+        if a == "--threads":
+            threads = int(next(it))
+        else:
+            names.append(a)
+    names = names or list(CASES)
+    fx_path = HERE / "fullsize.json"
+    fx = json.loads(fx_path.read_text()) if fx_path.exists() else {}
+    for name in names:
+        c = CASES[name]
+        with tempfile.TemporaryDirectory() as d:
+            d = Path(d)
+            snp = d / f"{name}.snp"
+            synth.write_snp_file(str(snp), synth.generate(**c["gen"]))
+            t0 = time.time()
+            subprocess.run([str(ORACLE), "-f", str(snp), "-o", str(d / "o.txt"), f"--n-threads={threads}",
+                            *c["opts"], f"--dump-points={d / 'o.dump'}"], check=True, capture_output=True)
+            dt = time.time() - t0
+            rows = read_dump(d / "o.dump")
+            fx[name] = dict(gen=c["gen"], options=c["opts"], input_sha256=sha256_file(snp),
+                            dump_sha256=canonical_dump(rows), out_sha256=sha256_file(d / "o.txt"),
+                            n_points=len(rows), sum_permute_n=sum(r[10] for r in rows),
+                            sample_every=97, sample=[canonical_row(r) for r in rows[::97]],
+                            oracle_s=round(dt, 1), oracle_threads=threads)
+        print(f"{name}: {len(rows)} points, oracle {dt:.1f} s on {threads} threads", flush=True)
+        fx_path.write_text(json.dumps(fx, indent=1) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

@@ -2,7 +2,7 @@
 
 usage: mr_worker.py <snpfile> <out> [options...]  (RANK/WORLD_SIZE/MASTER_* in env)
 Exchange over torch.distributed gloo (CPU tensors) so that two ranks can share
-one GPU; bench.py uses the nccl (RCCL) backend with one GPU per rank.
+one GPU, or (FSCL_MR_SHM=<name>) the library's own shared-memory exchange.
 """
 import os
 import sys
@@ -27,7 +27,10 @@ def main() -> int:
         t = torch.from_numpy(arr)  # shares memory with the C buffer
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
 
-    fscl_amd.set_ranks(rank, world, allreduce)
+    if os.environ.get("FSCL_MR_SHM"):  # the library's own shared-memory exchange
+        fscl_amd.set_ranks_shm(rank, world, os.environ["FSCL_MR_SHM"])
+    else:
+        fscl_amd.set_ranks(rank, world, allreduce)
     snp, out, opts = sys.argv[1], sys.argv[2], sys.argv[3:]
     fscl_amd.run(snp, out, **_kw(opts))
     st = fscl_amd.get_stats()

@@ -188,11 +188,15 @@ def test_search_maxalpha_dropin(built):
         assert (pt.lalpha.hex(), pt.sm_logl.hex(), pt.clr.hex()) == (row[3].hex(), row[4].hex(), row[2].hex())
 
 
-def test_two_ranks_on_one_gpu_match_one_rank(built, tmp):
-    """Parity mode with 2 processes (gloo exchange, both on GPU 0)."""
+@pytest.mark.parametrize("exchange", ["callback", "shm"])
+def test_two_ranks_on_one_gpu_match_one_rank(built, tmp, exchange):
+    """Parity mode with 2 processes (both on GPU 0): the exchange through a Python gloo
+    callback, or the library's own shared-memory all-gather."""
     c = manifest()["cases"]["g1_p25"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 1000), WORLD_SIZE="2",
-               FSCL_AMD_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+               FSCL_AMD_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0", FSCL_AMD_RANK_TIMEOUT="120")
+    if exchange == "shm":
+        env["FSCL_MR_SHM"] = f"/fscl_amd_mr_{os.getpid()}"
     procs = []
     for r in range(2):
         e = dict(env, RANK=str(r))
@@ -267,3 +271,79 @@ def test_full_size_configs_match_oracle(built, tmp, name, gen, opts):
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
     if name == "C5_chr":
         assert fscl_amd.get_stats()["window_ms"] > 0
+
+
+@pytest.fixture
+def two_contexts():
+    """This process drives GPU 0 through two device contexts (fscl_amd_set_devices)."""
+    fscl_amd.set_devices([0, 0])
+    yield
+    fscl_amd.set_device(0)
+
+
+@pytest.mark.parametrize("name,gen,opts", [
+    ("multi_chr", dict(n_chr=3, chr_len=6_000_000, snps_per_chr=6000, n=30, seed=91, sweeps_per_chr=1),
+     ["--coarse-grid-spacing=40000", "--n-permute=40"]),
+    ("windowed", dict(n_chr=2, chr_len=4_000_000, snps_per_chr=4000, n=30, seed=92, sweeps_per_chr=1),
+     ["--coarse-grid-spacing=40000", "--n-permute=6", "--eval-range=300"]),
+])
+def test_two_devices_in_one_process_match_oracle(built, tmp, two_contexts, name, gen, opts):
+    """Single-process multi-GPU (the CLI's --n-gpus): every batch split into two cost-balanced
+    shares on two contexts, one host permutation and pruning: bit-identical to the oracle."""
+    snp = tmp / f"{name}.snp"
+    synth.write_snp_file(str(snp), synth.generate(**gen))
+    er = [o for o in opts if o.startswith("--eval-range=")]
+    kw = _kw([o for o in opts if not o.startswith("--eval-range=")])
+    if er:
+        kw["eval_range"] = int(er[0].split("=")[1])
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=os.cpu_count() or 1)
+    fscl_amd.reset_stats()
+    scan = fscl_amd.run(snp, tmp / "g.txt", **kw)
+    assert fscl_amd.get_lib().fscl_amd_n_devices() == 2
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), name)
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+    assert fscl_amd.get_stats()["n_devices"] == 2
+
+
+def test_cli_n_gpus(built, tmp):
+    """fscl --n-gpus=1 and the CLI's default (every visible GPU) reproduce the golden output."""
+    c = manifest()["cases"]["g1_p25"]
+    env = {k: v for k, v in os.environ.items() if k != "FSCL_AMD_DEVICE"}
+    r = subprocess.run([str(CLI), "-f", str(GOLD / c["input"]), "-o", str(tmp / "o.txt"), "--n-gpus=1",
+                        *c["options"]], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr
+    assert (tmp / "o.txt").read_text() == (GOLD / "g1_p25.out").read_text()
+    r = subprocess.run([str(CLI), "-f", str(GOLD / c["input"]), "-o", str(tmp / "a.txt"), *c["options"]],
+                       capture_output=True, text=True, timeout=600, env=env)  # default: every visible GPU
+    assert r.returncode == 0, r.stderr
+    assert (tmp / "a.txt").read_text() == (GOLD / "g1_p25.out").read_text()
+
+
+def test_back_to_back_scan_permute_continue_the_stream(built, tmp):
+    """The rand() stream is seeded once per process (fscl.c:135) and continues across
+    scan_permute calls: two calls in a row equal the oracle driven the same way (counts
+    accumulate, scan-chromosome.c:488-498)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from oracle import OracleScan
+    snp = tmp / "b2b.snp"
+    synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=5_000_000, snps_per_chr=5000, n=30, seed=95,
+                                                  sweeps_per_chr=1))
+    orc = OracleScan(snp, threads=os.cpu_count() or 1, large_grid_sp=50000)
+    orc.reseed()
+    orc.scan()
+    orc.permute(8)
+    orc.permute(12)
+    want = orc.points()
+    fscl_amd.init_log_table()
+    fscl_amd.srand()
+    scan = fscl_amd.load_snp_input(snp)
+    fsp = fscl_amd.background_fsp(scan)
+    tab = fscl_amd.compute_sweep_model_tables(scan, fsp)
+    fscl_amd.compute_snp_null_model(scan, fsp)
+    fscl_amd.scan_chromosome(scan, tab, large_grid_sp=50000)
+    fscl_amd.scan_permute(scan, tab, 8, large_grid_sp=50000)
+    fscl_amd.scan_permute(scan, tab, 12, large_grid_sp=50000)
+    got = fscl_amd.points(scan)
+    assert [tuple(r) for r in got[["chr", "sweep_pos", "permute_p", "permute_n", "permute_finished"]].tolist()] == \
+        [(p[0], p[1], p[10], p[9], p[11]) for p in want]
+    assert [c.hex() for c in got["clr"]] == [p[2].hex() for p in want]

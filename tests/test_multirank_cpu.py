@@ -58,3 +58,67 @@ def test_int64_sum_exchange_preserves_bit_patterns(built, tmp_path):
         out, err = p.communicate(timeout=300)
         assert p.returncode == 0, err
         assert "ok" in out.split(), out
+
+
+SHM_WORKER = r"""
+import ctypes as C, os, sys
+import numpy as np
+sys.path.insert(0, os.environ["REPO"])
+import fscl_amd
+L = fscl_amd.get_lib()
+L.fh_shm_open.restype = C.c_void_p
+L.fh_shm_open.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_size_t]
+L.fh_shm_allgather.restype = C.c_int
+L.fh_shm_allgather.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int]
+L.fh_shm_close.argtypes = [C.c_void_p]
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+m = L.fh_shm_open(rank, world, os.environ["SHM_NAME"].encode(), 1 << 20)
+assert m, "attach"
+rng = np.random.default_rng(7)
+for it in range(200):  # many exchanges of varying sizes: both areas, every ordering
+    n = int(rng.integers(0, 300))
+    full = rng.integers(-2**62, 2**62, size=(n, 8), dtype=np.int64)  # 64-B items (fsclg_point_t)
+    cost = rng.random(n) + 0.01
+    lo, hi = fscl_amd.partition(cost, rank, world)
+    buf = np.zeros_like(full)
+    buf[lo:hi] = full[lo:hi]
+    assert L.fh_shm_allgather(m, buf.ctypes.data, 64, n, lo, hi) == 0
+    assert np.array_equal(buf, full), (rank, it)
+L.fh_shm_close(m)
+assert not os.path.exists("/dev/shm" + os.environ["SHM_NAME"])  # unlinked once all attached
+print("ok", rank)
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shared_memory_allgather(built, tmp_path, world):
+    """The library's own multi-process exchange (ranks.c): every rank writes its cost-balanced
+    contiguous share of a batch's 64-B results and reads the whole batch, 200 times over."""
+    script = tmp_path / "s.py"
+    script.write_text(SHM_WORKER)
+    env = dict(os.environ, WORLD_SIZE=str(world), REPO=str(ROOT), SHM_NAME=f"/fscl_amd_test_{os.getpid()}_{world}",
+               FSCL_AMD_RANK_TIMEOUT="60")
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(world)]
+    for p in procs:
+        out, err = p.communicate(timeout=300)
+        assert p.returncode == 0, err
+        assert "ok" in out.split(), out
+
+
+def test_device_shares_are_contiguous_and_cover(built):
+    """world * n_dev shares (rank r's local device l takes share r * n_dev + l): consecutive,
+    disjoint, covering, and each rank's devices form one contiguous range."""
+    import fscl_amd
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 7, 100, 5000):
+        cost = rng.random(n) * 10 + 0.1
+        for world, n_dev in ((1, 2), (2, 2), (2, 4), (4, 2), (1, 8)):
+            T = world * n_dev
+            spans = [fscl_amd.partition(cost, g, T) for g in range(T)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for a, b in zip(spans, spans[1:]):
+                assert a[1] == b[0] and a[0] <= a[1]
+            tot = cost.sum()
+            for lo, hi in spans:  # no share far above its part of the cost
+                assert cost[lo:hi].sum() <= tot / T + (cost.max() if n else 0) + 1e-9
