@@ -88,8 +88,17 @@ def cpu_info() -> dict:
             phys.add((cur.get("physical id"), cur.get("core id")))
     except OSError:
         pass
+    quota = None
+    try:  # cgroup v2 CPU bandwidth limit of this process (the GPU box's share of the node)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
     return {"cpu_model": model or platform.processor(), "node_logical_cpus": os.cpu_count(),
-            "node_physical_cores": len(phys) or None, "affinity_cpus": len(os.sched_getaffinity(0))}
+            "node_physical_cores": len(phys) or None, "affinity_cpus": aff, "cgroup_cpus": quota,
+            "usable_cpus": min(aff, quota) if quota else aff}
 
 
 def profile_summary(args) -> tuple[dict | None, str | None]:
@@ -317,7 +326,7 @@ def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, 
     """Returns (cpu_baseline dict, max |dCLR|, position mismatches)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     from oracle import OracleScan  # noqa: E402
-    threads = args.cpu_threads or info["affinity_cpus"]
+    threads = args.cpu_threads or info["usable_cpus"]  # every CPU this process may use (cgroup quota included)
     n_t = args.cpu_sample or max(64, min(gp, 24 * threads))
     n_1 = max(8, min(gp, 64))
     smp = _harness(snp, cfg, threads, n_t)

@@ -77,7 +77,7 @@ constexpr double LOG_AD_MAX = 4.0;    // fscl.h:80
 constexpr int PAD = 1024;             // slack after pos/row: a trip may read up to 64*U past a walk's end
 constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsigned order = signed order
 
-enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2 };
+enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2, PF_SPLIT_TIMEOUT = 4 };
 
 struct Params {
   const uint2* pr;             // [n_snps + PAD] (position ^ POS_BIAS, device row = caller's row + 1; 0: zero sentinel)
@@ -120,6 +120,12 @@ struct Params {
   int n_ep;
   fsclg_point_t* ept;          // mode 2 out / mode 0 in: evaluated endpoints
   const int2* cell_ep;         // mode 0: (start, end) endpoint indices of each cell, or null
+  // split cells (mode 0): `split` workgroups ("members") per cell share every walk's segments and
+  // combine their partial sums through a per-cell accumulator in global memory (XAcc, three
+  // regions used in turn, zeroed before the launch) and a per-cell arrival counter
+  int split;                   // members per cell (1: one workgroup per cell)
+  char* xacc;                  // [n_cells][3] XAcc
+  unsigned int* xcnt;          // [n_cells] arrivals
 };
 
 struct Pt {                     // one scan point being evaluated (scan_pt_t subset)
@@ -166,6 +172,24 @@ struct Smem {
   int word[MAXWALK];              // walks in segment order
   int hkey;                       // interval-histogram key of the phase: 0 coarse, 1 + c refine around coarse c
   unsigned long long tph[4];      // FSCLG_PHASE_TIMING: wall-clock ticks in bounds / layout / segments / resolve
+  int cell, member;               // split cells: this workgroup's cell and member index
+  int inst;                       // split cells: eval_walks instances so far (the XAcc region in turn)
+  int xbase;                      // split cells: this member's first tie slot
+  int xfail;                      // split cells: PF_SPLIT_TIMEOUT if a member never arrived
+};
+
+// a split cell's shared per-instance accumulator: integer sums add in any order (exact), the
+// segments' parity bits XOR (each segment has one member), the fp64 sums of lanes past 2^51 stay
+// per member and are added in member order (every member reads the same value)
+constexpr int MAXSPLIT = 8;
+struct XAcc {
+  unsigned long long P[MAXWALK], Q[MAXWALK];
+  double Pd[MAXSPLIT][MAXWALK], Qd[MAXSPLIT][MAXWALK];
+  unsigned int wflag[MAXWALK];
+  unsigned int segbits[MAXWALK][SEGWORDS];
+  unsigned int n_ties;
+  unsigned int pad;
+  int ties[MAXTIES];
 };
 
 // dynamic LDS of a workgroup (LDS = true): coefficient planes of the top K intervals, the
@@ -739,6 +763,108 @@ __device__ __forceinline__ void load_window(Smem& S, const Params& P, int wb) {
   if (threadIdx.x == 0) S.ivc0 = wb;
 }
 
+// agent-scope atomics: performed at the memory side, coherent across the XCDs' L2s
+__device__ __forceinline__ unsigned long long ag_add64(unsigned long long* p, unsigned long long v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned int ag_add32(unsigned int* p, unsigned int v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned int ag_or32(unsigned int* p, unsigned int v) {
+  return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned int ag_xor32(unsigned int* p, unsigned int v) {
+  return __hip_atomic_fetch_xor(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ag_xchg64(unsigned long long* p, unsigned long long v) {
+  return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Split cells: the members of a cell have each summed their segments of every walk into LDS;
+// add them up in the cell's XAcc region for this instance, meet at the cell's arrival counter,
+// and read the totals back, so that every member continues with identical values (resolve,
+// argmax and bisection then run redundantly and agree).  Every read of another member's data
+// is an atomic read-modify-write (add 0), served where the atomics were performed.  Member 0
+// zeroes the region of the previous instance (every member has read it before this
+// instance's arrival), in time for its reuse two instances later.  A member that waits
+// longer than ~1 s (the others never started: not co-resident) flags the cell and goes on.
+__device__ __noinline__ void combine_members(Smem& S, const Params& P, int nw) {
+  const int tid = threadIdx.x;
+  const int inst = S.inst;
+  XAcc* R = reinterpret_cast<XAcc*>(P.xacc + ((size_t)S.cell * 3 + (size_t)(inst % 3)) * sizeof(XAcc));
+  // 1. contribute
+  if (tid < nw) {
+    if (S.P[tid]) ag_add64(&R->P[tid], S.P[tid]);
+    if (S.Q[tid]) ag_add64(&R->Q[tid], S.Q[tid]);
+    if (S.wflag[tid]) {
+      ag_or32(&R->wflag[tid], 1u);
+      ag_xchg64(reinterpret_cast<unsigned long long*>(&R->Pd[S.member][tid]),
+                (unsigned long long)__double_as_longlong(S.Pd[tid]));
+      ag_xchg64(reinterpret_cast<unsigned long long*>(&R->Qd[S.member][tid]),
+                (unsigned long long)__double_as_longlong(S.Qd[tid]));
+    }
+    for (int j = 0; j < SEGWORDS; j++)
+      if (S.segbits[tid][j]) ag_xor32(&R->segbits[tid][j], S.segbits[tid][j]);
+  }
+  if (tid == 0) S.xbase = S.n_ties ? (int)ag_add32(&R->n_ties, (unsigned)S.n_ties) : 0;
+  __syncthreads();
+  {
+    const int nt = min(S.n_ties, MAXTIES), base = S.xbase;
+    for (int t = tid; t < nt; t += WG)
+      if (base + t < MAXTIES) __hip_atomic_exchange(&R->ties[base + t], S.ties[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // 2. arrive (release) and wait for every member (acquire)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned int* cnt = P.xcnt + S.cell;
+    ag_add32(cnt, 1u);
+    const unsigned int target = (unsigned)P.split * (unsigned)(inst + 1);
+    const unsigned long long t0 = wall_clock64();
+    while (ag_add32(cnt, 0u) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > 100000000ull) { S.xfail = PF_SPLIT_TIMEOUT; break; }  // ~1 s at 100 MHz
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 3. the totals
+  if (tid < nw) {
+    S.P[tid] = ag_add64(&R->P[tid], 0ull);
+    S.Q[tid] = ag_add64(&R->Q[tid], 0ull);
+    S.wflag[tid] = (int)ag_or32(&R->wflag[tid], 0u);
+    if (S.wflag[tid]) {
+      double pd = 0.0, qd = 0.0;
+      for (int m = 0; m < P.split; m++) {  // member order: the same sum on every member
+        pd += __longlong_as_double((long long)ag_add64(reinterpret_cast<unsigned long long*>(&R->Pd[m][tid]), 0ull));
+        qd += __longlong_as_double((long long)ag_add64(reinterpret_cast<unsigned long long*>(&R->Qd[m][tid]), 0ull));
+      }
+      S.Pd[tid] = pd; S.Qd[tid] = qd;
+    }
+    for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = ag_xor32(&R->segbits[tid][j], 0u);
+  }
+  if (tid == 0) S.xbase = (int)ag_add32(&R->n_ties, 0u);
+  __syncthreads();
+  {
+    const int nt = min(S.xbase, MAXTIES);
+    for (int t = tid; t < nt; t += WG) S.ties[t] = (int)ag_add32(reinterpret_cast<unsigned int*>(&R->ties[t]), 0u);
+  }
+  __syncthreads();
+  if (tid == 0) S.n_ties = S.xbase;  // the total: above MAXTIES marks the overflow as before
+  // 4. member 0 clears the previous instance's region (read by every member before this arrival)
+  if (S.member == 0) {
+    XAcc* Z = reinterpret_cast<XAcc*>(P.xacc + ((size_t)S.cell * 3 + (size_t)((inst + 2) % 3)) * sizeof(XAcc));
+    unsigned int* z = reinterpret_cast<unsigned int*>(Z);
+    for (int k = tid; k < (int)(sizeof(XAcc) / 4); k += WG)
+      __hip_atomic_exchange(z + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0) S.inst = inst + 1;
+  __syncthreads();
+}
+
 template <bool LDS>
 __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -830,7 +956,9 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
        __syncthreads();
      }
      const int ge = __builtin_amdgcn_readfirstlane(S.gseg[gi + 1]);
-     for (int g = __builtin_amdgcn_readfirstlane(S.gseg[gi]) + wave; g < ge; g += NWAVE) {
+     const int mstride = NWAVE * P.split;  // split cells: the members deal the segments round-robin
+     for (int g = __builtin_amdgcn_readfirstlane(S.gseg[gi]) + __builtin_amdgcn_readfirstlane(S.member) * NWAVE + wave;
+          g < ge; g += mstride) {
       while (k < nw - 1 && g >= S.w[S.word[k]].seg0 + S.w[S.word[k]].nseg) k++;  // walks own consecutive segment ranges
       const int w = S.word[k];
       if (w != cw) {  // the wave's segments of one walk are consecutive: flush once per walk
@@ -843,6 +971,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
   }
   __syncthreads();
+  if (P.split > 1) combine_members(S, P, nw);
   PHASE_MARK(2);
   TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk(S, tid);
@@ -978,10 +1107,13 @@ template <bool LDS>
 __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P) {
   __shared__ Smem S;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous run of cells
-  // cells arrive in the host's longest-first order; the hardware dispatches blocks in order
-  // (round-robin over the XCDs), so the long cells start first and spread over the XCDs
-  const int cell = blockIdx.x;
+  // cells arrive in the host's longest-first order (XCD-aware: blocks b and b + 8 share an
+  // XCD); the hardware dispatches blocks in order (round-robin over the XCDs), so the long
+  // cells start first and spread over the XCDs.  Split cells: the members of cell c are blocks
+  // (c / 8) * 8G + 8m + c % 8, m < G -- one XCD's L2 holds the cell's sites
+  const int G = P.split, b = (int)blockIdx.x;
+  const int cell = G > 1 ? (b / (8 * G)) * 8 + (b & 7) : b;
+  const int member = G > 1 ? (b >> 3) % G : 0;
   if (cell >= P.n_cells) return;
   if (P.mode == 0 && P.cells[cell].chr < 0) {  // idle block of the host's XCD placement
     if (P.ctrace && tid < 8) P.ctrace[8 * cell + tid] = 0;
@@ -989,7 +1121,8 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
   }
   if (tid < 8) S.cnt[tid] = 0;
   if (tid < 4) S.tph[tid] = 0;
-  if (P.ctrace && tid == 0) { P.ctrace[8 * cell] = wall_clock64(); P.ctrace[8 * cell + 2] = __smid(); }
+  if (tid == 0) { S.cell = cell; S.member = member; S.inst = 0; S.xfail = 0; }
+  if (P.ctrace && tid == 0 && member == 0) { P.ctrace[8 * cell] = wall_clock64(); P.ctrace[8 * cell + 2] = __smid(); }
   if constexpr (LDS) {
     double* thr = reinterpret_cast<double*>(fsclg_dyn + P.off_thr);
     double* nul = reinterpret_cast<double*>(fsclg_dyn + P.off_nul);
@@ -1048,17 +1181,18 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
       }
       __syncthreads();
     }
-    if (tid == 0) {  // one store of the result (P.out may be host memory: no read-modify-write)
+    if (tid == 0 && member == 0) {  // one store of the result (P.out may be host memory: no read-modify-write)
       const Pt& r = S.pt[0].clr > S.pt[1].clr ? S.pt[0] : S.pt[1];
       fsclg_point_t o;
       write_point(o, r);
-      o.flags |= S.pt[0].flags | S.pt[1].flags;
+      o.flags |= S.pt[0].flags | S.pt[1].flags | S.xfail;
       o.cost = (uint32_t)min(S.cnt[0] >> 10, 0xFFFFFFFFull);
       P.out[cell] = o;
       S.cnt[7] += 1;
     }
   }
   __syncthreads();
+  if (member != 0) return;  // split cells: member 0 reports (the others counted the same walks)
   if (tid < 8 && S.cnt[tid]) atomicAdd(&P.stats[tid], S.cnt[tid]);
   if (P.ctrace && tid == 0) {
     P.ctrace[8 * cell + 1] = wall_clock64(); P.ctrace[8 * cell + 3] = S.cnt[0];
@@ -1192,6 +1326,12 @@ struct Batch {
   std::vector<int2> epos, ucell_ep;
   int n_cells = 0, nu = 0, nlaunch = 0, slot = -1;
   bool pending = false;
+  int split_max = 1;                // fsclg_set_batch_split
+  int split = 1;                    // members per cell of the current launch
+  char* d_xacc = nullptr;           // split cells' accumulators and arrival counters
+  unsigned int* d_xcnt = nullptr;
+  size_t xacc_cap = 0;
+  int xcnt_cap = 0;
 };
 
 struct fsclg_ctx {
@@ -1348,6 +1488,8 @@ int fsclg_close(fsclg_ctx* c) {
   }
   for (Batch& B : c->batch) {
     if (B.d_ept) hipFree(B.d_ept);
+    if (B.d_xacc) hipFree(B.d_xacc);
+    if (B.d_xcnt) hipFree(B.d_xcnt);
     for (void* p : {(void*)B.p_cells, (void*)B.p_out, (void*)B.p_epos, (void*)B.p_cell_ep, (void*)B.p_ctrace})
       if (p) hipHostFree(p);
     hipEventDestroy(B.ev0);
@@ -1753,6 +1895,7 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
+  P.split = 1; P.xacc = nullptr; P.xcnt = nullptr;
   if (getenv("FSCLG_CELL_TRACE")) {
     if (B.ctrace_cap < n) {
       if (B.p_ctrace) hipHostFree(B.p_ctrace);
@@ -1868,7 +2011,18 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
     B.ucell_ep[u] = make_int2(e[0], e[1]);
   }
   const int ne = (int)B.epos.size();
-  const bool use_ep = !getenv("FSCLG_NO_DEDUP") && (2 * nu - ne) * 8 >= nu;  // saves >= 1/8 of the endpoint work
+  // split cells: a batch of few cells (the permutation pipeline's blocking batch in the
+  // pruned tail) gives each cell up to split_max workgroups, within a budget of workgroups
+  // that stays below half of the device's resident slots, so that every member of a cell is
+  // resident together while other batches run (their workgroups never wait on anything)
+  int G = 1;
+  if (B.split_max > 1) {
+    static const int budget = getenv("FSCLG_SPLIT_BUDGET") ? atoi(getenv("FSCLG_SPLIT_BUDGET")) : 256;
+    G = std::min(std::min(B.split_max, MAXSPLIT), budget / std::max(nu, 1));
+    if (G < 2) G = 1;
+  }
+  B.split = G;
+  const bool use_ep = G == 1 && !getenv("FSCLG_NO_DEDUP") && (2 * nu - ne) * 8 >= nu;  // saves >= 1/8 of the endpoint work
   // XCD placement of the endpoint launch (two endpoints per block, blocks dealt round-robin
   // over the XCDs): in (chromosome, position) order, the blocks x, x + 8, ... of class x take
   // one consecutive run of endpoints, as the cells below
@@ -1984,7 +2138,20 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
     P.ept = B.d_ept; P.cell_ep = B.p_cell_ep;
     c->n_ep_saved += (unsigned long long)(2 * nu - ne);
   }
-  if ((r = launch_blocks(B.stream, P, nl))) return r;
+  if (G > 1) {
+    const size_t xb = (size_t)nl * 3 * sizeof(XAcc);
+    if (B.xacc_cap < xb) {
+      if (B.d_xacc) hipFree(B.d_xacc);
+      B.d_xacc = nullptr; B.xacc_cap = 0;
+      HIPCHK(hipMalloc((void**)&B.d_xacc, xb), "hipMalloc split accumulators");
+      B.xacc_cap = xb;
+    }
+    if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, nl))) return r;
+    HIPCHK(hipMemsetAsync(B.d_xacc, 0, xb, B.stream), "hipMemsetAsync");
+    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");
+    P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
+  }
+  if ((r = launch_blocks(B.stream, P, G > 1 ? (nl + 7) / 8 * 8 * G : nl))) return r;
   HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
   HIPCHK(hipEventRecord(B.ev2, B.stream), "hipEventRecord");
   B.traced = P.ctrace != nullptr;
@@ -2037,7 +2204,16 @@ int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
     if (B.p_cells[k].chr >= 0) c->cell_cost[cell_key(B.p_cells[k])] = B.p_out[k].cost;
   for (int i = 0; i < B.n_cells; i++) out[i] = B.p_out[B.upos[B.uidx[i]]];
   for (int i = 0; i < B.n_cells; i++)
-    if (out[i].flags) return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL, "device flag");
+    if (out[i].flags)
+      return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL,
+                     out[i].flags & PF_SPLIT_TIMEOUT ? "device flag: a split cell's members were not resident together"
+                                                     : "device flag");
+  return FSCLG_OK;
+}
+
+int fsclg_set_batch_split(fsclg_ctx* c, int batch, int max_members) {
+  if (!c || batch < 0 || batch >= NBATCH || max_members < 1) return set_err(FSCLG_E_ARG, "batch split");
+  c->batch[batch].split_max = std::min(max_members, MAXSPLIT);
   return FSCLG_OK;
 }
 

@@ -247,6 +247,12 @@ static void dev_open(void) {
              fsclg_last_error());
     D.dev[l] = D.want_dev[l];
     D.n_dev = l + 1;
+    /* batch 0 -- the initial scan and the permutation pipeline's blocking batch: when it has
+       few cells, each gets several workgroups (FSCL_AMD_SPLIT members, default 8; 1 = off) */
+    {
+      const char *e = getenv("FSCL_AMD_SPLIT");
+      dev_check(fsclg_set_batch_split(D.ctx[l], 0, e ? (atoi(e) < 1 ? 1 : atoi(e)) : 8), "batch split");
+    }
   }
   if (n > 1) logmsg(MSG_STATUS, "fscl_amd: %d GPUs in this process", n);
 }

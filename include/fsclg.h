@@ -145,6 +145,13 @@ int fsclg_set_chr_null(fsclg_ctx *c, const double *chr_null);
 int fsclg_set_alpha_grid(fsclg_ctx *c, const double *coarse, int n_coarse, const double *refine,
                          const int32_t *n_refine);
 
+/* Split cells: a launch of batch `batch` with few cells gives each cell up to max_members
+   (<= 8) workgroups that share its walks' segments (default 1).  For latency, not throughput:
+   the pipeline's blocking batch, whose result orders the next trial.  The members of a cell
+   are resident together (a budget of 256 workgroups per launch, below the device's resident
+   slots); a cell whose members were not fails with FSCLG_E_KERNEL. */
+int fsclg_set_batch_split(fsclg_ctx *c, int batch, int max_members);
+
 /* batched search_maxpos over n_cells cells; blocks until out[] is written */
 int fsclg_search_maxpos(fsclg_ctx *c, const fsclg_cell_t *cells, int n_cells, int eval_range, int bp_resl,
                         fsclg_point_t *out);
