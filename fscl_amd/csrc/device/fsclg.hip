@@ -62,8 +62,9 @@ constexpr int NWAVE = WG / 64;
 #define FSCLG_SEG 4096
 #endif
 constexpr int SEG = FSCLG_SEG;     // terms per work segment
+constexpr int SEG_SPLIT = 1024;    // split cells (latency): finer segments spread over the members' waves
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
-constexpr int MAXSEG_W = (163841 / SEG + 2 + 31) / 32 * 32;  // segments per walk (42 at 163841 terms)
+constexpr int MAXSEG_W = (163841 / SEG_SPLIT + 2 + 31) / 32 * 32;  // segments per walk (163 at 163841 terms, split)
 constexpr int SEGWORDS = MAXSEG_W / 32;
 constexpr int MAXTIES = 512;       // per eval_walks; overflow sends the affected argmax to the exact slow path
 constexpr int MAXREF = 16;
@@ -483,16 +484,18 @@ __device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, 
 // [nearest - nl, nearest] (walked downwards, sm-search.c:122-128) and right part
 // [nearest + 1, nearest + nr] are cut into separate SEG-site segments (left ones first), so
 // each part's walk order is monotone in the index.
+template <int SEGN>
 __device__ __forceinline__ void seg_bounds(const Walk& W, const Pt& pt, int s, int& ib, int& ie) {
   const int lo = pt.nearest - W.nl, near = pt.nearest, hi = pt.nearest + W.nr;
-  if (s < W.nsl) { ib = lo + s * SEG; ie = min(ib + SEG, near + 1); }
-  else { ib = near + 1 + (s - W.nsl) * SEG; ie = min(ib + SEG, hi + 1); }
+  if (s < W.nsl) { ib = lo + s * SEGN; ie = min(ib + SEGN, near + 1); }
+  else { ib = near + 1 + (s - W.nsl) * SEGN; ie = min(ib + SEGN, hi + 1); }
 }
 
 // the segment of site index i of the walk
+template <int SEGN>
 __device__ __forceinline__ int seg_of(const Walk& W, const Pt& pt, int i) {
   const int lo = pt.nearest - W.nl, near = pt.nearest;
-  return i <= near ? (i - lo) / SEG : W.nsl + (i - near - 1) / SEG;
+  return i <= near ? (i - lo) / SEGN : W.nsl + (i - near - 1) / SEGN;
 }
 
 __device__ __forceinline__ bool odd_int(double v) { return v - 2.0 * floor(0.5 * v) != 0.0; }
@@ -521,7 +524,7 @@ __device__ __forceinline__ double uniform_f64(double v) {
 // window or the global table, a uniform branch).  Otherwise the trip takes the per-lane path
 // of run_segment and re-centres civ on its last site.  Only the final trip of a segment
 // masks lanes past its end (zero sentinel row).
-template <bool LDS>
+template <bool LDS, int SEGN>
 __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Params& P, int lane, double& acc,
                                                 double& accm) {
   const Walk& W = S.w[w];
@@ -530,7 +533,7 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
   const double la = W.la, inv = pt.inv_u;
   const int lo = pt.nearest - W.nl;
   int ib, ie;
-  seg_bounds(W, pt, s, ib, ie);
+  seg_bounds<SEGN>(W, pt, s, ib, ie);
   const int n = ie - ib;
   const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
   const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
@@ -678,6 +681,7 @@ __device__ __forceinline__ void flush_walk(Smem& S, int w, double acc, double ac
 // resolve walk w's exact value (thread per walk).  S.P = sum R, S.Q = sum |R| over the walk.
 // Ties are replayed in k order: fl(acc + t) rounds to even, so where t/u = F + 1/2 an odd
 // running sum takes the other neighbour of the even R (+1 if R = F, -1 if R = F + 1).
+template <int SEGN>
 __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[W.p];
@@ -713,7 +717,7 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
       // order = (left tie) the left part after it, (right tie) the left part and the
       // right part before it; R of a tie is even, so both read lpar ^ prefix-in-part
       const int jj = bestv & 0x3FFFF;
-      const int sg = seg_of(W, pt, pt.nearest - nl + jj);
+      const int sg = seg_of<SEGN>(W, pt, pt.nearest - nl + jj);
       int sp = 0;
       for (int t = (jj <= nl ? 0 : nsl); t < sg; t++) sp ^= segbit(t);
       const int pre = (bestv >> 18) & 1, up = (bestv >> 19) & 1;
@@ -788,7 +792,7 @@ __device__ __forceinline__ unsigned long long ag_xchg64(unsigned long long* p, u
 // zeroes the region of the previous instance (every member has read it before this
 // instance's arrival), in time for its reuse two instances later.  A member that waits
 // longer than ~1 s (the others never started: not co-resident) flags the cell and goes on.
-__device__ __noinline__ void combine_members(Smem& S, const Params& P, int nw) {
+__device__ __forceinline__ void combine_members(Smem& S, const Params& P, int nw) {
   const int tid = threadIdx.x;
   const int inst = S.inst;
   XAcc* R = reinterpret_cast<XAcc*>(P.xacc + ((size_t)S.cell * 3 + (size_t)(inst % 3)) * sizeof(XAcc));
@@ -865,8 +869,9 @@ __device__ __noinline__ void combine_members(Smem& S, const Params& P, int nw) {
   __syncthreads();
 }
 
-template <bool LDS>
+template <bool LDS, bool SPLIT>
 __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
+  constexpr int SEGN = SPLIT ? SEG_SPLIT : SEG;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nw = __builtin_amdgcn_readfirstlane(S.nwalk);
 #ifdef FSCLG_PHASE_TIMING
@@ -902,7 +907,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
       const int near = S.pt[W.p].nearest, lo = near - W.nl, hi = near + W.nr;
       int nsl;
       if (!len) { nsl = 0; nseg = 0; }
-      else { nsl = (W.nl + SEG) / SEG; nseg = nsl + (W.nr + SEG - 1) / SEG; }
+      else { nsl = (W.nl + SEGN) / SEGN; nseg = nsl + (W.nr + SEGN - 1) / SEGN; }
       W.len = len; W.wb = wb; W.nsl = nsl; W.nseg = nseg;
     }
     // walks in descending window base, stable: each walk's rank and first segment
@@ -956,25 +961,26 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
        __syncthreads();
      }
      const int ge = __builtin_amdgcn_readfirstlane(S.gseg[gi + 1]);
-     const int mstride = NWAVE * P.split;  // split cells: the members deal the segments round-robin
-     for (int g = __builtin_amdgcn_readfirstlane(S.gseg[gi]) + __builtin_amdgcn_readfirstlane(S.member) * NWAVE + wave;
-          g < ge; g += mstride) {
+     // split cells: the members deal the segments round-robin
+     const int mstride = SPLIT ? NWAVE * P.split : NWAVE;
+     const int g0 = SPLIT ? __builtin_amdgcn_readfirstlane(S.member) * NWAVE + wave : wave;
+     for (int g = __builtin_amdgcn_readfirstlane(S.gseg[gi]) + g0; g < ge; g += mstride) {
       while (k < nw - 1 && g >= S.w[S.word[k]].seg0 + S.w[S.word[k]].nseg) k++;  // walks own consecutive segment ranges
       const int w = S.word[k];
       if (w != cw) {  // the wave's segments of one walk are consecutive: flush once per walk
         if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
         cw = w; acc = 0.0; accm = 0.0;
       }
-      run_segment_idx<LDS>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+      run_segment_idx<LDS, SEGN>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
      }
     }
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
   }
   __syncthreads();
-  if (P.split > 1) combine_members(S, P, nw);
+  if constexpr (SPLIT) combine_members(S, P, nw);
   PHASE_MARK(2);
   TRACE("  segments done: ties=%d\n", S.n_ties);
-  if (tid < nw) resolve_walk(S, tid);
+  if (tid < nw) resolve_walk<SEGN>(S, tid);
   if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;
   __syncthreads();
   PHASE_MARK(3);
@@ -1006,7 +1012,7 @@ __device__ __forceinline__ int argmax_or_mark(Smem& S, int first, int count, dou
 }
 
 // search_maxalpha for the points in slots [p0, p0+np) (sm-search.c:269-300)
-template <bool LDS>
+template <bool LDS, bool SPLIT = false>
 __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < np) set_binade(S.pt[p0 + tid]);
@@ -1021,7 +1027,7 @@ __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, in
   if (tid == 0) { S.nwalk = np * P.n_coarse; S.cnt[3] += np; S.hkey = 0; }
   __syncthreads();
   for (int phase = 0; phase < 2; phase++) {
-    eval_walks<LDS>(S, P);
+    eval_walks<LDS, SPLIT>(S, P);
     // argmax per point, with slow-path settling
     for (int round = 0; round < 2; round++) {
       if (tid == 0) {
@@ -1098,7 +1104,7 @@ __device__ __forceinline__ void write_point(fsclg_point_t& o, const Pt& pt) {
   o.lalpha = pt.la; o.null_logl = pt.N; o.sm_logl = pt.sm; o.clr = pt.clr;
 }
 
-template <bool LDS>
+template <bool LDS, bool SPLIT>
 #ifdef FSCLG_WPE  // waves per SIMD to budget registers for (caps VGPRs at 512 / FSCLG_WPE)
 #define FSCLG_KATTR __attribute__((amdgpu_waves_per_eu(FSCLG_WPE, FSCLG_WPE)))
 #else
@@ -1111,7 +1117,7 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
   // XCD); the hardware dispatches blocks in order (round-robin over the XCDs), so the long
   // cells start first and spread over the XCDs.  Split cells: the members of cell c are blocks
   // (c / 8) * 8G + 8m + c % 8, m < G -- one XCD's L2 holds the cell's sites
-  const int G = P.split, b = (int)blockIdx.x;
+  const int G = SPLIT ? P.split : 1, b = (int)blockIdx.x;
   const int cell = G > 1 ? (b / (8 * G)) * 8 + (b & 7) : b;
   const int member = G > 1 ? (b >> 3) % G : 0;
   if (cell >= P.n_cells) return;
@@ -1161,7 +1167,7 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
       if (wave < 2) init_point_wave(S.pt[wave], c.chr, wave == 0 ? c.start_pos : c.end_pos, P, lane);
       __syncthreads();
       if (tid == 0) S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps);
-      search_maxalpha_pts<LDS>(S, P, 0, 2);  // start and end points share the two phases
+      search_maxalpha_pts<LDS, SPLIT>(S, P, 0, 2);  // start and end points share the two phases
     }
     int iter = 0;
     for (;;) {
@@ -1173,7 +1179,7 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
         if (lane == 0) S.cnt[1] += (unsigned long long)S.pt[2].n_snps;
       }
       __syncthreads();
-      search_maxalpha_pts<LDS>(S, P, 2, 1);
+      search_maxalpha_pts<LDS, SPLIT>(S, P, 2, 1);
       if (tid == 0) {
         // scan-chromosome.c:116: compare exactly as written
         if ((S.pt[0].clr + S.pt[2].clr) >= (S.pt[1].clr + S.pt[2].clr)) S.pt[1] = S.pt[2];
@@ -1446,8 +1452,21 @@ int fsclg_open(int device, fsclg_ctx** out) {
   int lo = 0, hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
   HIPCHK(hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, hi), "hipStreamCreate");
-  for (int k = 0; k < 3; k++)
-    HIPCHK(hipStreamCreateWithPriority(&c->bstream[k], hipStreamNonBlocking, k == 0 ? hi : lo), "hipStreamCreate");
+  // FSCLG_RESERVE=r (experiment): the bulk streams leave every r-th CU to the blocking batch's
+  // high-priority stream (r = 4: a quarter of the CUs), whose workgroups then find free slots
+  const int reserve = getenv("FSCLG_RESERVE") ? atoi(getenv("FSCLG_RESERVE")) : 0;
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+  for (int k = 0; k < 3; k++) {
+    if (k > 0 && reserve > 1) {
+      std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
+      for (int cu = 0; cu < prop.multiProcessorCount; cu++)
+        if (cu % reserve != reserve - 1) mask[cu / 32] |= 1u << (cu % 32);
+      HIPCHK(hipExtStreamCreateWithCUMask(&c->bstream[k], (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+    } else {
+      HIPCHK(hipStreamCreateWithPriority(&c->bstream[k], hipStreamNonBlocking, k == 0 ? hi : lo), "hipStreamCreate");
+    }
+  }
   for (int b = 0; b < NBATCH; b++) {
     Batch& B = c->batch[b];
     B.stream = c->bstream[b < 2 ? 0 : 1 + (b & 1)];
@@ -1845,6 +1864,7 @@ static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
 static void plan_cache(fsclg_ctx* c) {
   c->plan_dirty = false;
   c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
+  if (getenv("FSCLG_NO_WINDOW")) return;  // experiment: every coefficient from the global table
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0);
   if (room < 32 || c->n_iv <= 0 || c->h_pos.empty() || c->h_coarse.empty() || c->h_lt3.empty()) return;
@@ -1919,13 +1939,17 @@ static int launch_blocks(hipStream_t stream, const Params& P, int n) {
     int dev = 0;
     HIPCHK(hipGetDevice(&dev), "hipGetDevice");
     if (dev >= 64 || !(attr_set >> dev & 1ull)) {
-      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true>),
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true, false>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true, true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
       if (dev < 64) attr_set |= 1ull << dev;
     }
-    hipLaunchKernelGGL(search_maxpos_kernel<true>, dim3(grid), dim3(WG), dyn, stream, P);
+    if (P.split > 1) hipLaunchKernelGGL((search_maxpos_kernel<true, true>), dim3(grid), dim3(WG), dyn, stream, P);
+    else hipLaunchKernelGGL((search_maxpos_kernel<true, false>), dim3(grid), dim3(WG), dyn, stream, P);
   } else
-    hipLaunchKernelGGL(search_maxpos_kernel<false>, dim3(grid), dim3(WG), 0, stream, P);
+    if (P.split > 1) hipLaunchKernelGGL((search_maxpos_kernel<false, true>), dim3(grid), dim3(WG), 0, stream, P);
+    else hipLaunchKernelGGL((search_maxpos_kernel<false, false>), dim3(grid), dim3(WG), 0, stream, P);
   HIPCHK(hipGetLastError(), "launch search_maxpos_kernel");
   return FSCLG_OK;
 }
@@ -1970,7 +1994,7 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
   for (int i = 0; i < n_cells; i++) {
     if (cells[i].chr < 0 || cells[i].chr >= c->n_chr) return set_err(FSCLG_E_ARG, "cell chromosome");
     const long long nwin = std::min((long long)c->h_chr_n[cells[i].chr], 2ll * eval_range + 1);
-    if (nwin / SEG + 2 > (long long)MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
+    if (nwin / SEG_SPLIT + 2 > (long long)MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
   }
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
@@ -2150,6 +2174,11 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
     HIPCHK(hipMemsetAsync(B.d_xacc, 0, xb, B.stream), "hipMemsetAsync");
     HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");
     P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
+    // latency: no LDS coefficient windows (their loads, repeated by every member for every
+    // phase, cost more than the global gathers of a lightly loaded device)
+    P.ivc0 = 0; P.n_civ = 0; P.civ_max = 0; P.n_cache = 0;
+    P.off_thr = 0; P.off_nul = (c->n_iv + 1) * 8;
+    P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8;
   }
   if ((r = launch_blocks(B.stream, P, G > 1 ? (nl + 7) / 8 * 8 * G : nl))) return r;
   HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
@@ -2238,7 +2267,7 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
     if (p.window_start < 0 || p.window_end >= c->n_snps || p.window_start > p.window_end ||
         p.nearest_snp < p.window_start || p.nearest_snp > p.window_end)
       return set_err(FSCLG_E_ARG, "point window");
-    if ((p.window_end - p.window_start + 1) / SEG + 2 > MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
+    if ((p.window_end - p.window_start + 1) / SEG_SPLIT + 2 > MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
   }
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;

@@ -851,11 +851,14 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   tb_reserve(&A, n_act ? n_act : 1);
   for (k = 0; k < K; k++) tb_reserve(&Bt[k], n_act ? n_act : 1);
   for (i = 0; i < n_act; i++) act[i] = i;
+  FILE *tt = getenv("FSCL_AMD_TRIAL_TRACE") ? fopen(getenv("FSCL_AMD_TRIAL_TRACE"), "w") : NULL;  /* development aid */
+  double tr[8];
   for (;;) {
     const int slot = (trial + 1) % K;
     trial_batch_t *B = &Bt[slot];
     double tp = fh_now();
     uint32_t *prow;
+    tr[0] = tp;
     /* the slot's previous trial: its bulk results (no draws among them) */
     if (B->submitted) {
       tb_wait(B, pq);
@@ -863,6 +866,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     }
     D.st.search_s += fh_now() - tp;
     tp = fh_now();
+    tr[1] = tp;
     prow = slot_stage(slot);
     block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g);
     D.st.host_perm_s += fh_now() - tp;
@@ -873,6 +877,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     cr_logmsg(MSG_STATUS, "Scanning snp block permutations... %7d (%d scan pts remaining)        ", trial, n_act);
     if (n_act == 0 || trial > n_perm) break;
     tp = fh_now();
+    tr[2] = tp;
     chr_null_sums(prow, nul[slot]);
     D.st.host_null_s += fh_now() - tp;
     tp = fh_now();
@@ -899,11 +904,14 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     D.st.n_crit += (unsigned long long)A.n;
     /* both batches always go through submit / wait (an empty share is a no-op), so that
        every rank takes part in the same exchanges */
+    tr[3] = fh_now();
     tb_submit(&A, slot, eval_range, bp_resl);
     tb_submit(B, slot, eval_range, bp_resl);
     {
       int drain = 0;
+      tr[4] = fh_now();
       tb_wait(&A, pq);
+      tr[5] = fh_now();
       /* a point that may draw in this trial needs every earlier result applied first */
       for (k = 0; k < A.n && !drain; k++) {
         const int a = A.pt[k];
@@ -927,6 +935,11 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     done = trial;
     D.st.search_s += fh_now() - tp;
     D.st.trials++;
+    if (tt) /* trial, active, blocking cells, bulk cells; us: bulk wait, permute, null sums + upload + build,
+               submit, blocking wait, flush */
+      fprintf(tt, "%d %d %d %d %.0f %.0f %.0f %.0f %.0f %.0f\n", trial, n_act, A.n, B->n, (tr[1] - tr[0]) * 1e6,
+              (tr[2] - tr[1]) * 1e6, (tr[3] - tr[2]) * 1e6, (tr[4] - tr[3]) * 1e6, (tr[5] - tr[4]) * 1e6,
+              (fh_now() - tr[5]) * 1e6);
     if (g_sigint) sigint_dump(s, n_perm);
   }
   /* the bulk batches still in flight, oldest first */
@@ -942,6 +955,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   }
   for (i = 0; i < s->n_scan_pts; i++)
     if (pq[i].n) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline: unapplied results");
+  if (tt) fclose(tt);
   tb_free(&A);
   for (k = 0; k < K; k++) { tb_free(&Bt[k]); free(nul[k]); }
   free(act); free(pq);
