@@ -13,6 +13,7 @@ fixtures of make_golden.py) and store, in fullsize.json,
     python tests/golden/make_fullsize.py [case ...] [--threads N]
 
 Cases (SURVEY §8(d) / BASELINE.json):
+  C4_full_p2  22 x 45k SNPs (1.0M), n=200, --n-permute=2         (configs[3] genome)
   C5_full     22 x 227k SNPs (5.0M), n=400, initial scan          (configs[4] genome)
   C5_chr_p200 one C5 chromosome, --n-permute=200 (early prune)    (configs[4] regime)
 """
@@ -36,6 +37,8 @@ from fscl_amd import synth  # noqa: E402
 from util import ORACLE, read_dump  # noqa: E402
 
 CASES = {
+    "C4_full_p2": dict(gen=dict(n_chr=22, chr_len=45_454_545, snps_per_chr=45_455, n=200, seed=44, sweeps_per_chr=2),
+                       opts=["--n-permute=2"]),
     "C5_full": dict(gen=dict(n_chr=22, chr_len=227_272_727, snps_per_chr=227_273, n=400, seed=55, sweeps_per_chr=2),
                     opts=[]),
     "C5_chr_p200": dict(gen=dict(n_chr=1, chr_len=227_272_727, snps_per_chr=227_273, n=400, seed=57,

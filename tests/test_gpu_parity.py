@@ -11,7 +11,8 @@ import sys
 import numpy as np
 import pytest
 
-from util import CLI, GOLD, ROOT, assert_rows_equal, manifest, points_rows, read_dump, run_oracle
+from util import (CLI, GOLD, ROOT, assert_rows_equal, manifest, points_rows, read_dump, run_oracle,
+                  usable_cpus)
 import fscl_amd
 from fscl_amd import synth
 
@@ -77,7 +78,7 @@ def test_cli_matches_golden(built, tmp, case):
 def test_gpu_matches_oracle(built, tmp, name, gen, opts):
     snp = tmp / f"{name}.snp"
     synth.write_snp_file(str(snp), synth.generate(**gen))
-    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
     assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), name)
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
@@ -104,8 +105,7 @@ def test_windowed_null_sums_match_oracle(built, tmp, name, er, parts, opts):
     for p in parts:
         chrs += synth.generate(**p)
     synth.write_snp_file(str(snp), chrs)
-    run_oracle(snp, tmp / "o.txt", [*opts, f"--eval-range={er}"], tmp / "o.dump",
-               threads=min(16, os.cpu_count() or 1))
+    run_oracle(snp, tmp / "o.txt", [*opts, f"--eval-range={er}"], tmp / "o.dump")
     fscl_amd.reset_stats()
     scan = fscl_amd.run(snp, tmp / "g.txt", eval_range=er, **_kw(opts))
     assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), name)
@@ -125,7 +125,7 @@ def test_shared_cells_and_endpoints_match_oracle(built, tmp):
     snp = tmp / "shared.snp"
     synth.write_snp_file(str(snp), chrs)
     opts = ["--coarse-grid-spacing=50000", "--n-permute=6"]
-    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
     assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), "shared")
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
@@ -143,7 +143,7 @@ def test_tiny_chromosomes_match_oracle(built, tmp):
     snp = tmp / "tiny.snp"
     synth.write_snp_file(str(snp), chrs)
     opts = ["--coarse-grid-spacing=20000", "--n-permute=5"]
-    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
     assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), "tiny")
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
@@ -220,7 +220,7 @@ def test_pipelined_trials_match_lockstep_and_oracle(built, tmp, monkeypatch):
     synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=8_000_000, snps_per_chr=8000, n=30, seed=81,
                                                   sweeps_per_chr=2))
     opts = ["--coarse-grid-spacing=40000", "--n-permute=70"]
-    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     fscl_amd.reset_stats()
     scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
     st = fscl_amd.get_stats()
@@ -239,7 +239,7 @@ def test_c2_scale_scan_and_short_permutation(built, tmp):
     snp = tmp / "c2.snp"
     synth.write_config(str(snp), "C2", seed=1)
     opts = ["--n-permute=2"]
-    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
     pts = fscl_amd.points(scan)
     assert len(pts) == 2000
@@ -264,12 +264,47 @@ def test_full_size_configs_match_oracle(built, tmp, name, gen, opts):
     bit-exact against the oracle (positions, windows, lalpha, sm_logl, CLR, counts)."""
     snp = tmp / f"{name}.snp"
     synth.write_snp_file(str(snp), synth.generate(**gen))
-    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=min(16, os.cpu_count() or 1))
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     fscl_amd.reset_stats()
     scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
     assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), name)
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
     if name == "C5_chr":
+        assert fscl_amd.get_stats()["window_ms"] > 0
+
+
+def _fullsize():
+    import json
+    return json.loads((GOLD / "fullsize.json").read_text())
+
+
+@pytest.mark.parametrize("name", sorted(_fullsize()))
+def test_full_genomes_match_oracle_fixture(built, tmp, name):
+    """Full-size BASELINE genomes whose oracle run is too slow for the box
+    (tests/golden/make_fullsize.py ran it here and stored digests):
+      C4_full_p2  configs[3]'s whole 22-chromosome 1.0M-SNP genome, n=200, 3 trials;
+      C5_full     configs[4]'s whole 5.0M-SNP genome, n=400, initial scan;
+      C5_chr_p200 one C5 chromosome at 200 permutations: the early-prune regime
+                  (points cross permute_p >= 20 and draw, scan-chromosome.c:488-498).
+    Bit-exact: SHA-256 of every field of every point (floats as hex) and of the output."""
+    sys.path.insert(0, str(GOLD))
+    from make_fullsize import canonical_dump, canonical_row, sha256_file
+    fx = _fullsize()[name]
+    snp = tmp / f"{name}.snp"
+    synth.write_snp_file(str(snp), synth.generate(**fx["gen"]))
+    assert sha256_file(snp) == fx["input_sha256"], "synthetic input differs from the fixture's"
+    fscl_amd.reset_stats()
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(fx["options"]))
+    rows = points_rows(fscl_amd.points(scan))
+    assert len(rows) == fx["n_points"]
+    assert sum(r[10] for r in rows) == fx["sum_permute_n"]
+    if canonical_dump(rows) != fx["dump_sha256"]:
+        k = fx["sample_every"]
+        for i, want in enumerate(fx["sample"]):
+            assert canonical_row(rows[i * k]) == want, f"{name}: point {i * k}"
+        pytest.fail(f"{name}: dump digest differs (the sampled rows agree)")
+    assert sha256_file(tmp / "g.txt") == fx["out_sha256"]
+    if name.startswith("C5"):
         assert fscl_amd.get_stats()["window_ms"] > 0
 
 
@@ -296,7 +331,7 @@ def test_two_devices_in_one_process_match_oracle(built, tmp, two_contexts, name,
     kw = _kw([o for o in opts if not o.startswith("--eval-range=")])
     if er:
         kw["eval_range"] = int(er[0].split("=")[1])
-    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump", threads=os.cpu_count() or 1)
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     fscl_amd.reset_stats()
     scan = fscl_amd.run(snp, tmp / "g.txt", **kw)
     assert fscl_amd.get_lib().fscl_amd_n_devices() == 2
@@ -328,7 +363,7 @@ def test_back_to_back_scan_permute_continue_the_stream(built, tmp):
     snp = tmp / "b2b.snp"
     synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=5_000_000, snps_per_chr=5000, n=30, seed=95,
                                                   sweeps_per_chr=1))
-    orc = OracleScan(snp, threads=os.cpu_count() or 1, large_grid_sp=50000)
+    orc = OracleScan(snp, threads=usable_cpus(), large_grid_sp=50000)
     orc.reseed()
     orc.scan()
     orc.permute(8)

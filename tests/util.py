@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import json
+import os
 import subprocess
 from pathlib import Path
 
@@ -34,8 +35,22 @@ def points_rows(pts) -> list[tuple]:
     return [tuple(p[k].item() for k in DUMP_FIELDS) for p in pts]
 
 
-def run_oracle(snp, out, opts, dump=None, threads: int = 1) -> subprocess.CompletedProcess:
-    cmd = [str(ORACLE), "-f", str(snp), "-o", str(out), f"--n-threads={threads}", *opts]
+def usable_cpus() -> int:
+    """CPUs this process may run on: the affinity mask, capped by the cgroup v2 CPU quota
+    (a GPU box's share of its node)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def run_oracle(snp, out, opts, dump=None, threads: int | None = None) -> subprocess.CompletedProcess:
+    """The oracle CLI; threads default to every CPU this process may use."""
+    cmd = [str(ORACLE), "-f", str(snp), "-o", str(out), f"--n-threads={threads or usable_cpus()}", *opts]
     if dump:
         cmd.append(f"--dump-points={dump}")
     return subprocess.run(cmd, capture_output=True, text=True, check=True)
