@@ -130,7 +130,10 @@ def issue_roofline(prof: dict) -> dict | None:
     if not f64:  # static share of FP64 VALU in the term loop when not collected
         f64 = valu * prof.get("fp64_valu_share", 0.5)
         f64_src = f"static FP64 share {prof.get('fp64_valu_share', 0.5)} of VALU (DESIGN.md §4.6)"
-    clk = pmc.get("GRBM_GUI_ACTIVE", 0) / 8 / (tr["avg_ms"] * 1e-3) if pmc.get("GRBM_GUI_ACTIVE") else 2.4e9
+    # effective clock (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE / 8 XCDs / dispatch time) over the
+    # counter pass's own dispatches, which rocprofv3 serializes (the trace's overlap excluded)
+    d_ms = prof.get("pmc_dispatch_ms", {}).get("sq")
+    clk = pmc["GRBM_GUI_ACTIVE"] / 8 / (d_ms * 1e-3) if pmc.get("GRBM_GUI_ACTIVE") and d_ms else 2.4e9
     cycles_used = 2 * (valu - f64) + 4 * f64
     cycles_avail = N_SIMD * clk * tu["busy_ms_per_launch"] * 1e-3
     out = {"bound": "valu-issue", "achieved": cycles_used / (tu["busy_ms_per_launch"] * 1e-3) / 1e12,

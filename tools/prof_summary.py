@@ -38,19 +38,23 @@ if kt.exists():
     out["trace_union"] = {"calls": len(iv), "busy_ms": busy / 1e6,
                           "busy_ms_per_launch": busy / 1e6 / max(1, len(iv)),
                           "sum_ms": sum(e0 - s0 for s0, e0 in iv) / 1e6}
-pmc = {}
-for grp in ("fetch", "write", "sq"):
+pmc, pmc_ms = {}, {}
+for grp in ("fetch", "write", "sq", "f64"):
     f = src / grp / "run_counter_collection.csv"
     if not f.exists():
         continue
-    agg, n = defaultdict(float), defaultdict(int)
+    agg, n, dur = defaultdict(float), defaultdict(int), {}
     for r in csv.DictReader(open(f)):
         if "search_maxpos" in r["Kernel_Name"]:
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
             n[r["Counter_Name"]] += 1
+            dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     for k in agg:
         pmc[k] = agg[k] / n[k]
+    if dur:  # counter passes serialize the dispatches: each one's own duration, no overlap
+        pmc_ms[grp] = sum(dur.values()) / len(dur) / 1e6
 out["pmc_per_launch"] = pmc
+out["pmc_dispatch_ms"] = pmc_ms
 if "FETCH_SIZE" in pmc:
     fetch = pmc["FETCH_SIZE"] * 1024 * 2  # KB; x2: gfx950 FETCH_SIZE counts half of wide coalesced reads
     write = pmc.get("WRITE_SIZE", 0.0) * 1024
