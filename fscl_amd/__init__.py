@@ -81,7 +81,9 @@ class Stats(C.Structure):  # fscl_amd_stats_t
                 ("host_upload_s", C.c_double), ("search_s", C.c_double), ("prune_s", C.c_double),
                 ("n_dup_cells", C.c_ulonglong), ("n_ep_saved", C.c_ulonglong), ("busy_ms", C.c_double),
                 ("wait_s", C.c_double), ("n_crit", C.c_ulonglong), ("n_drain", C.c_ulonglong),
-                ("n_devices", C.c_int)]
+                ("n_devices", C.c_int), ("spec_threads", C.c_int), ("spec_posted", C.c_ulonglong),
+                ("spec_hits", C.c_ulonglong), ("spec_cands", C.c_ulonglong), ("spec_wait_s", C.c_double),
+                ("spec_done", C.c_ulonglong), ("spec_gen_s", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -11,9 +11,12 @@
  * rank replays the same host logic and evaluates a cost-balanced contiguous
  * share of the cells; one int64 sum-allreduce per trial assembles the CLRs.
  */
+#define _GNU_SOURCE
 #include <errno.h>
 #include <float.h>
 #include <math.h>
+#include <pthread.h>
+#include <sched.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -611,13 +614,19 @@ void scan_chromosome(scan_t *s, sm_ptable_t *sm, int eval_range, int bp_resl, in
    chromosome) are swapped into place; positions never move.  Q9: a block
    running past the end is shifted left (j -= k - n) instead of indexing
    p[-m] as the reference does; such events are counted. */
-static void block_permute(uint32_t *prow, const uint32_t *row, const snp_t *snps, int n, double nbp,
-                          double width_mb, fh_rand_t *g) {
+static int block_permute(uint32_t *prow, const uint32_t *row, const snp_t *snps, int n, double nbp,
+                         double width_mb, fh_rand_t *g, unsigned long long *negj, const volatile unsigned *gen,
+                         unsigned my_gen) {
   int i = 0, j, k;
   const double width = width_mb * 1e6;
-  memcpy(prow, row, sizeof(uint32_t) * n);
+  for (i = 0; i < n; i += 1 << 18) { /* in 1 MB pieces: a cancelled candidate stops soon */
+    if (gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1;
+    memcpy(prow + i, row + i, sizeof(uint32_t) * (size_t)(n - i < (1 << 18) ? n - i : 1 << 18));
+  }
+  i = 0;
   while (i < n) {
     const int r1 = fh_rand(g), r2 = fh_rand(g);
+    if (gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1; /* speculation cancelled */
     j = r1 / (2147483647 + 1.0) * n;
     if (r2 == 0) k = n; /* Q10: log(0) */
     else k = j + (int)(-1.0 / nbp * log(r2 / (2147483647 + 1.0)));
@@ -637,7 +646,7 @@ static void block_permute(uint32_t *prow, const uint32_t *row, const snp_t *snps
       k = lo;
     }
     if (i + (k - j) >= n) k = n;
-    if (k > n) { D.st.negj++; j -= k - n; k = n; }
+    if (k > n) { (*negj)++; j -= k - n; k = n; }
     {
       /* scan-chromosome.c:365-372: swap p[i++] with p[j++] while j < k and i < n; disjoint
          ranges in one vectorisable pass, overlapping ones element by element as written */
@@ -660,6 +669,42 @@ static void block_permute(uint32_t *prow, const uint32_t *row, const snp_t *snps
       }
     }
   }
+  return 0;
+}
+
+/* chr_null_sums on one thread: four chromosomes' sequential sums interleaved (independent
+   chains, each in the reference's order; four accumulators hide the add latency) */
+static int chr_null_sums_1t(const uint32_t *row, double *out, const volatile unsigned *gen, unsigned my_gen) {
+  const double *nr = D.nullrow;
+  int c = 0, t, t1, k;
+  for (; c < D.n_chr; c += 4) {
+    const int nc = D.n_chr - c < 4 ? D.n_chr - c : 4;
+    const uint32_t *r[4];
+    double a[4] = {0., 0., 0., 0.};
+    int m = 1 << 30;
+    for (k = 0; k < 4; k++) {
+      r[k] = row + D.chr_start[c + (k < nc ? k : 0)];
+      if (k < nc && D.chr_n[c + k] < m) m = D.chr_n[c + k];
+    }
+    for (t1 = 0; t1 < m; t1 += 8192) {
+      const int te = m - t1 < 8192 ? m : t1 + 8192;
+      double a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+      const uint32_t *r0 = r[0], *r1 = r[1], *r2 = r[2], *r3 = r[3];
+      if (__atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1; /* cancelled */
+      for (t = t1; t < te; t++) { /* chains k >= nc repeat chain 0 and are dropped */
+        a0 += nr[r0[t]];
+        a1 += nr[r1[t]];
+        a2 += nr[r2[t]];
+        a3 += nr[r3[t]];
+      }
+      a[0] = a0; a[1] = a1; a[2] = a2; a[3] = a3;
+    }
+    for (k = 0; k < nc; k++) {
+      for (t = m; t < D.chr_n[c + k]; t++) a[k] += nr[r[k][t]];
+      out[c + k] = a[k];
+    }
+  }
+  return 0;
 }
 
 /* one trial's rows (in D.stage[slot]) and null sums to the slot on every local device;
@@ -670,11 +715,12 @@ static uint32_t *slot_stage(int slot) {
   return D.stage[slot];
 }
 
-static void slot_upload(int slot, const double *nul) {
+static void slot_upload_buf(int slot, const uint32_t *rows, const double *nul) {
   int l;
-  for (l = 0; l < D.n_dev; l++)
-    dev_check(fsclg_slot_set_rows_host(D.ctx[l], slot, D.stage[slot], nul), "set rows");
+  for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_set_rows_host(D.ctx[l], slot, rows, nul), "set rows");
 }
+
+static void slot_upload(int slot, const double *nul) { slot_upload_buf(slot, D.stage[slot], nul); }
 
 static volatile sig_atomic_t g_sigint = 0;
 static struct timeval g_last_dump;
@@ -704,6 +750,226 @@ static void sigint_dump(scan_t *s, int n_perm) {
     if (fn) output_clr_null_distribution(fn, s);
   }
   gettimeofday(&g_last_dump, NULL);
+}
+
+/* ------------------------------------------------ speculative permutations
+   (SURVEY §8(f) row 1).  The reference builds each trial's permutation serially from the
+   rand() stream after the previous trial's prune draws (scan-chromosome.c:441-456, 488-498),
+   and so does this host: trial t+1's permutation starts at the state S left by trial t's own
+   permutation, advanced by d_t draws -- one per hit of a point whose permute_p is already
+   >= 19.  d_t is known only when trial t's results are in, but its distribution is
+   predictable from those points' hit rates.  So while the GPUs evaluate trial t, worker
+   threads build the permutations (and whole-chromosome null sums) for the most likely d_t,
+   each from its own copy of S; when d_t is known the matching candidate is taken (its end
+   state becomes the stream's) and the others are cancelled; a miss builds it on the main
+   thread as before.  The stream, and so every result, is unchanged.  Before any point can
+   draw (the first 19 trials) d_t = 0 is certain: one candidate, never a miss. */
+#define SPEC_MAX 32
+#define PB_FREE (-1)
+#define PB_CAND (-2)
+#define PB_HELD (-3)
+
+typedef struct {
+  uint32_t *buf;   /* one trial's rows, pinned: every local device's upload reads it */
+  double *nul;     /* its whole-chromosome null sums */
+  int owner;       /* the row slot whose upload reads it, or PB_FREE / PB_CAND / PB_HELD */
+} pbuf_t;
+
+static struct {
+  pthread_t th[SPEC_MAX];
+  int n_th;
+  pthread_mutex_t mu;
+  pthread_cond_t cv, done;
+  volatile unsigned gen;  /* bumped to cancel the posted candidates */
+  int stop;
+  fh_rand_t base;         /* the posted job: S, and the draw counts to build */
+  int n_job, next, running;
+  int d[SPEC_MAX], bi[SPEC_MAX], state[SPEC_MAX];  /* 0 queued, 1 running, 2 done, 3 cancelled */
+  fh_rand_t end[SPEC_MAX];
+  unsigned long long negj[SPEC_MAX];
+  const snp_t *snps;      /* the permutation's inputs (fixed while a job is posted) */
+  int n;
+  double nbp, width_mb;
+  pbuf_t pb[FSCLG_N_SLOTS + 2 * SPEC_MAX + 1];
+  int n_pb, pb_cap, pb_nchr;
+} SP = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
+
+static void *spec_worker(void *arg) {
+  (void)arg;
+  pthread_mutex_lock(&SP.mu);
+  for (;;) {
+    while (!SP.stop && SP.next >= SP.n_job) pthread_cond_wait(&SP.cv, &SP.mu);
+    if (SP.stop) break;
+    {
+      const int c = SP.next++;
+      const unsigned my = SP.gen;
+      const int d = SP.d[c];
+      pbuf_t *b = SP.pb + SP.bi[c];
+      fh_rand_t r = SP.base;
+      unsigned long long negj = 0;
+      int t, ok;
+      SP.state[c] = 1;
+      SP.running++;
+      pthread_mutex_unlock(&SP.mu);
+      const double t0 = fh_now();
+      for (t = 0; t < d; t++) (void)fh_rand(&r);
+      ok = block_permute(b->buf, D.row, SP.snps, SP.n, SP.nbp, SP.width_mb, &r, &negj, &SP.gen, my) == 0 &&
+           chr_null_sums_1t(b->buf, b->nul, &SP.gen, my) == 0;
+      pthread_mutex_lock(&SP.mu);
+      SP.running--;
+      if (ok && SP.gen == my) {
+        SP.state[c] = 2; SP.end[c] = r; SP.negj[c] = negj;
+        D.st.spec_gen_s += fh_now() - t0;
+        D.st.spec_done++;
+      }
+      else { /* cancelled: its buffer is free again (index c may already belong to a newer job) */
+        if (SP.gen == my) SP.state[c] = 3;
+        b->owner = PB_FREE;
+      }
+      pthread_cond_broadcast(&SP.done);
+    }
+  }
+  pthread_mutex_unlock(&SP.mu);
+  return NULL;
+}
+
+/* CPUs this process may use (affinity, capped by the cgroup v2 quota) */
+static int usable_cpus(void) {
+  cpu_set_t cs;
+  int n = 1;
+  FILE *f;
+  if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+  if ((f = fopen("/sys/fs/cgroup/cpu.max", "r"))) {
+    char q[32];
+    long per = 0;
+    if (fscanf(f, "%31s %ld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+      const long c = atol(q) / per;
+      if (c >= 1 && c < n) n = (int)c;
+    }
+    fclose(f);
+  }
+  return n;
+}
+
+/* worker threads: FSCL_AMD_SPEC, else this process's share of the usable CPUs (one process
+   per GPU shares the node: LOCAL_WORLD_SIZE) less the main thread */
+static int spec_threads_wanted(void) {
+  const char *e = getenv("FSCL_AMD_SPEC"), *lw = getenv("LOCAL_WORLD_SIZE");
+  int n = e ? atoi(e) : usable_cpus() / (lw && atoi(lw) > 0 ? atoi(lw) : 1) - 1;
+  return n < 0 ? 0 : n > SPEC_MAX ? SPEC_MAX : n;
+}
+
+static void spec_start(void) {
+  const int want = spec_threads_wanted();
+  while (SP.n_th < want) {
+    if (pthread_create(&SP.th[SP.n_th], NULL, spec_worker, NULL) != 0) break;
+    SP.n_th++;
+  }
+}
+
+static void spec_stop(void) {
+  int t;
+  pthread_mutex_lock(&SP.mu);
+  SP.stop = 1;
+  SP.gen++;
+  pthread_cond_broadcast(&SP.cv);
+  pthread_mutex_unlock(&SP.mu);
+  for (t = 0; t < SP.n_th; t++) pthread_join(SP.th[t], NULL);
+  SP.n_th = 0;
+  SP.stop = 0;
+  for (t = 0; t < SP.n_pb; t++) { fsclg_host_free(SP.pb[t].buf); free(SP.pb[t].nul); }
+  SP.n_pb = SP.pb_cap = SP.pb_nchr = 0;
+}
+
+/* buffers for K slots, the candidates and the main thread's own (no job posted) */
+static void pb_reserve(int n_snps, int K) {
+  const int want = K + 2 * SP.n_th + 1;
+  int b;
+  if (SP.pb_cap < n_snps || SP.pb_nchr < D.n_chr) {
+    for (b = 0; b < SP.n_pb; b++) { fsclg_host_free(SP.pb[b].buf); free(SP.pb[b].nul); }
+    SP.n_pb = 0;
+    SP.pb_cap = n_snps;
+    SP.pb_nchr = D.n_chr;
+  }
+  for (; SP.n_pb < want; SP.n_pb++) {
+    pbuf_t *p = SP.pb + SP.n_pb;
+    p->buf = fsclg_host_alloc(sizeof(uint32_t) * (size_t)(SP.pb_cap ? SP.pb_cap : 1));
+    if (!p->buf) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
+    p->nul = fh_malloc(sizeof(double) * (SP.pb_nchr ? SP.pb_nchr : 1), "null sums");
+  }
+  for (b = 0; b < SP.n_pb; b++) SP.pb[b].owner = PB_FREE;
+}
+
+static int pb_get(void) {
+  int b;
+  for (b = 0; b < SP.n_pb; b++)
+    if (SP.pb[b].owner == PB_FREE) { SP.pb[b].owner = PB_HELD; return b; }
+  logmsg(MSG_FATAL, "fscl_amd: no free permutation buffer");
+  return -1;
+}
+
+/* the slot's last upload has read its buffer on every local device: free it */
+static void slot_release(int slot) {
+  int l, b;
+  for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_wait(D.ctx[l], slot), "slot wait");
+  for (b = 0; b < SP.n_pb; b++) if (SP.pb[b].owner == slot) SP.pb[b].owner = PB_FREE;
+}
+
+/* no candidate running (cancelled ones included): the buffers are the caller's again */
+static void spec_quiesce(void) {
+  pthread_mutex_lock(&SP.mu);
+  SP.gen++;
+  SP.n_job = SP.next = 0;
+  while (SP.running) pthread_cond_wait(&SP.done, &SP.mu);
+  pthread_mutex_unlock(&SP.mu);
+}
+
+/* build candidates for the draw counts dl[0..nd) from stream state *g */
+static void spec_post(const fh_rand_t *g, const int *dl, int nd) {
+  int c;
+  pthread_mutex_lock(&SP.mu);
+  SP.base = *g;
+  for (c = 0; c < nd; c++) {
+    int b;
+    for (b = 0; b < SP.n_pb && SP.pb[b].owner != PB_FREE; b++) {}
+    if (b == SP.n_pb) break;
+    SP.pb[b].owner = PB_CAND;
+    SP.d[c] = dl[c]; SP.bi[c] = b; SP.state[c] = 0;
+  }
+  SP.next = 0;
+  SP.n_job = c;
+  SP.gen++;
+  pthread_cond_broadcast(&SP.cv);
+  pthread_mutex_unlock(&SP.mu);
+  D.st.spec_posted++;
+  D.st.spec_cands += (unsigned long long)c;
+}
+
+/* the candidate for d draws (its end state into *g), or -1; the others are cancelled and
+   their buffers freed */
+static int spec_take(int d, fh_rand_t *g) {
+  int c, hit = -1, bi = -1;
+  pthread_mutex_lock(&SP.mu);
+  for (c = 0; c < SP.n_job; c++) if (SP.d[c] == d) hit = c;
+  if (hit >= 0) {
+    const double t0 = fh_now();
+    while (SP.state[hit] < 2) pthread_cond_wait(&SP.done, &SP.mu);
+    D.st.spec_wait_s += fh_now() - t0;
+    if (SP.state[hit] == 2) {
+      *g = SP.end[hit];
+      D.st.negj += SP.negj[hit];
+      bi = SP.bi[hit];
+      SP.pb[bi].owner = PB_HELD;
+      D.st.spec_hits++;
+    }
+  }
+  /* cancel the rest without waiting: a running one frees its buffer when it stops */
+  for (c = 0; c < SP.n_job; c++)
+    if (c != hit && SP.state[c] != 1 && SP.pb[SP.bi[c]].owner == PB_CAND) SP.pb[SP.bi[c]].owner = PB_FREE;
+  SP.gen++;
+  SP.n_job = SP.next = 0;
+  pthread_mutex_unlock(&SP.mu);
+  return bi;
 }
 
 /* ------------------------------------------------ pipelined permutation trials
@@ -810,6 +1076,8 @@ static void tb_wait(trial_batch_t *b, pqueue_t *pq) {
 
 /* apply point i's queued results in trial order, up to trial `upto`; only trial `draw`
    may draw rand() (scan-chromosome.c:488-502) */
+static unsigned long long g_draws;  /* rand() draws of the pruning pass so far */
+
 static void pq_flush(scan_t *s, pqueue_t *pq, int i, int upto, int draw, fh_rand_t *g, int save) {
   pqueue_t *q = pq + i;
   scan_pt_t *p = s->scan_pts + i;
@@ -820,6 +1088,7 @@ static void pq_flush(scan_t *s, pqueue_t *pq, int i, int upto, int draw, fh_rand
       p->permute_p++;
       if (p->permute_p >= 20) {
         if (e->trial != draw) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline: out-of-order rand draw");
+        g_draws++;
         if (p->permute_p / (double)p->permute_n >= fh_rand(g) / (2147483647 + 1.0))
           p->permute_finished = 1; /* Q7: ratio uses the pre-increment count */
       }
@@ -831,6 +1100,38 @@ static void pq_flush(scan_t *s, pqueue_t *pq, int i, int upto, int draw, fh_rand
     q->head = (q->head + 1) % PQ;
     q->n--;
   }
+}
+
+/* the most likely draw counts of the trial whose blocking batch is A (into dl, at most nmax):
+   every point that may draw hits with probability ~ its hit rate so far; d is their sum, taken
+   as normal -- a window of integers around the mean, 3.3 sigma each side */
+static int spec_candidates(const scan_t *s, const pqueue_t *pq, const trial_batch_t *A, int nmax, int *dl) {
+  double mu = 0., var = 0.;
+  int m = 0, k, lo, nd;
+  for (k = 0; k < A->n; k++) {
+    const scan_pt_t *q = s->scan_pts + A->pt[k];
+    if (q->permute_p + pq[A->pt[k]].n >= 20) {
+      const double h = (q->permute_p + 1.0) / (q->permute_n + 2.0);
+      mu += h;
+      var += h * (1. - h);
+      m++;
+    }
+  }
+  if (m == 0) { dl[0] = 0; return 1; }
+  nd = 2 * (int)ceil(3.3 * sqrt(var)) + 1;
+  if (nd > nmax) nd = nmax;
+  if (nd > m + 1) nd = m + 1;
+  lo = (int)floor(mu + 0.5) - nd / 2;
+  if (lo + nd - 1 > m) lo = m - nd + 1;
+  if (lo < 0) lo = 0;
+  for (k = 0; k < nd; k++) dl[k] = lo + k;
+  for (k = 1; k < nd; k++) { /* most likely first: free workers take them in this order */
+    const int v = dl[k];
+    int b = k;
+    for (; b > 0 && fabs(dl[b - 1] - mu) > fabs(v - mu); b--) dl[b] = dl[b - 1];
+    dl[b] = v;
+  }
+  return nd;
 }
 
 static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eval_range, int bp_resl,
@@ -853,6 +1154,12 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   for (i = 0; i < n_act; i++) act[i] = i;
   FILE *tt = getenv("FSCL_AMD_TRIAL_TRACE") ? fopen(getenv("FSCL_AMD_TRIAL_TRACE"), "w") : NULL;  /* development aid */
   double tr[8];
+  unsigned long long draw_mark = 0;
+  int posted = 0, from_spec, bi;
+  spec_start();
+  D.st.spec_threads = SP.n_th;
+  pb_reserve(s->n_snps, K);
+  SP.snps = s->snps; SP.n = s->n_snps; SP.nbp = permute_nbp; SP.width_mb = scan_width_mb;
   for (;;) {
     const int slot = (trial + 1) % K;
     trial_batch_t *B = &Bt[slot];
@@ -867,8 +1174,16 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     D.st.search_s += fh_now() - tp;
     tp = fh_now();
     tr[1] = tp;
-    prow = slot_stage(slot);
-    block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g);
+    slot_release(slot);
+    /* this trial's permutation: the candidate for the previous trial's draw count, else built here */
+    bi = posted ? spec_take((int)(g_draws - draw_mark), g) : -1;
+    from_spec = bi >= 0;
+    if (bi < 0) {
+      bi = pb_get();
+      block_permute(SP.pb[bi].buf, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
+    }
+    SP.pb[bi].owner = slot;
+    prow = SP.pb[bi].buf;
     D.st.host_perm_s += fh_now() - tp;
     trial++;
     for (i = k = 0; i < n_act; i++)
@@ -878,10 +1193,11 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     if (n_act == 0 || trial > n_perm) break;
     tp = fh_now();
     tr[2] = tp;
-    chr_null_sums(prow, nul[slot]);
+    if (!from_spec) chr_null_sums(prow, SP.pb[bi].nul);  /* a candidate carries its own */
     D.st.host_null_s += fh_now() - tp;
+    memcpy(nul[slot], SP.pb[bi].nul, sizeof(double) * (D.n_chr ? D.n_chr : 1));
     tp = fh_now();
-    slot_upload(slot, nul[slot]);
+    slot_upload_buf(slot, prow, nul[slot]);
     D.st.host_upload_s += fh_now() - tp;
     tp = fh_now();
     A.n = B->n = 0;
@@ -907,8 +1223,16 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     tr[3] = fh_now();
     tb_submit(&A, slot, eval_range, bp_resl);
     tb_submit(B, slot, eval_range, bp_resl);
+    /* while the GPUs work: the next trial's permutation for this trial's likely draw counts */
+    posted = SP.n_th > 0;
+    if (posted) {
+      int dl[SPEC_MAX];
+      spec_post(g, dl, spec_candidates(s, pq, &A, SP.n_th, dl));
+    }
+    draw_mark = g_draws;
     {
-      int drain = 0;
+      int drain = 0, m = 0;
+      for (k = 0; k < A.n; k++) m += s->scan_pts[A.pt[k]].permute_p + pq[A.pt[k]].n >= 20;
       tr[4] = fh_now();
       tb_wait(&A, pq);
       tr[5] = fh_now();
@@ -931,15 +1255,16 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
         }
       }
       for (k = 0; k < A.n; k++) pq_flush(s, pq, A.pt[k], trial, trial, g, save); /* ascending point order */
+      tr[6] = m; tr[7] = (double)(g_draws - draw_mark);
     }
     done = trial;
     D.st.search_s += fh_now() - tp;
     D.st.trials++;
     if (tt) /* trial, active, blocking cells, bulk cells; us: bulk wait, permute, null sums + upload + build,
-               submit, blocking wait, flush */
-      fprintf(tt, "%d %d %d %d %.0f %.0f %.0f %.0f %.0f %.0f\n", trial, n_act, A.n, B->n, (tr[1] - tr[0]) * 1e6,
-              (tr[2] - tr[1]) * 1e6, (tr[3] - tr[2]) * 1e6, (tr[4] - tr[3]) * 1e6, (tr[5] - tr[4]) * 1e6,
-              (fh_now() - tr[5]) * 1e6);
+               submit, blocking wait, flush; points that could draw, draws */
+      fprintf(tt, "%d %d %d %d %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n", trial, n_act, A.n, B->n,
+              (tr[1] - tr[0]) * 1e6, (tr[2] - tr[1]) * 1e6, (tr[3] - tr[2]) * 1e6, (tr[4] - tr[3]) * 1e6,
+              (tr[5] - tr[4]) * 1e6, (fh_now() - tr[5]) * 1e6, tr[6], tr[7]);
     if (g_sigint) sigint_dump(s, n_perm);
   }
   /* the bulk batches still in flight, oldest first */
@@ -955,6 +1280,8 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   }
   for (i = 0; i < s->n_scan_pts; i++)
     if (pq[i].n) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline: unapplied results");
+  for (k = 0; k < K; k++) slot_release(k);  /* every upload has read its buffer */
+  spec_quiesce();
   if (tt) fclose(tt);
   tb_free(&A);
   for (k = 0; k < K; k++) { tb_free(&Bt[k]); free(nul[k]); }
@@ -996,7 +1323,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   for (;;) {
     double tp = fh_now();
     prow = slot_stage(0);
-    block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g);
+    block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
     D.st.host_perm_s += fh_now() - tp;
     trial++;
     for (i = k = 0; i < n_act; i++)
@@ -1275,6 +1602,7 @@ void fscl_amd_reset_stats(void) {
 }
 
 void fscl_amd_shutdown(void) {
+  spec_stop();
   dev_close_all();
   if (DI.ctx) fsclg_close(DI.ctx);
   free(DI.null_full); free(DI.null_seen); free(DI.pos); free(DI.row); free(DI.tpos); free(DI.trow);

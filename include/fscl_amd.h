@@ -202,6 +202,13 @@ typedef struct {
   unsigned long long n_crit;  /* scan_permute: cells in the trials' blocking (near-critical) batches */
   unsigned long long n_drain; /* scan_permute: trials that had to wait for every bulk batch in flight */
   int n_devices;          /* local GPUs this process drives */
+  int spec_threads;       /* scan_permute: permutation worker threads (0: no speculation) */
+  unsigned long long spec_posted; /* trials whose next permutation was generated ahead, per draw count */
+  unsigned long long spec_hits;   /*   of which the draw count was among the candidates */
+  unsigned long long spec_cands;  /*   candidates generated */
+  double spec_wait_s;     /* host time waiting for the chosen candidate to finish */
+  unsigned long long spec_done; /* candidates completed (not cancelled) */
+  double spec_gen_s;      /* worker seconds spent on the completed candidates */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);
