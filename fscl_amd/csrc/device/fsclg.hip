@@ -977,8 +977,8 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
   }
   __syncthreads();
+  PHASE_MARK(2);  // FSCLG_PHASE_TIMING: slot 3 holds the members' combine and the resolve
   if constexpr (SPLIT) combine_members(S, P, nw);
-  PHASE_MARK(2);
   TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk<SEGN>(S, tid);
   if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;

@@ -724,11 +724,12 @@ static void slot_upload(int slot, const double *nul) { slot_upload_buf(slot, D.s
 
 static volatile sig_atomic_t g_sigint = 0;
 static struct timeval g_last_dump;
-static void on_sigint(int sig) { /* scan-chromosome.c:553-560 */
+static double g_sigint_window = 10.;  /* seconds; FSCL_AMD_SIGINT_WINDOW_MS (tests) shortens it */
+static void on_sigint(int sig) { /* scan-chromosome.c:557-569 */
   struct timeval now;
   (void)sig;
   gettimeofday(&now, NULL);
-  if ((now.tv_sec - g_last_dump.tv_sec) + (now.tv_usec - g_last_dump.tv_usec) / 1e6 < 10) {
+  if ((now.tv_sec - g_last_dump.tv_sec) + (now.tv_usec - g_last_dump.tv_usec) / 1e6 < g_sigint_window) {
     static const char msg[] = "\nanother interrupt signal received, aborting permutation\n";
     if (write(2, msg, sizeof msg - 1) < 0) {}
     _exit(255);
@@ -1265,7 +1266,19 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       fprintf(tt, "%d %d %d %d %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n", trial, n_act, A.n, B->n,
               (tr[1] - tr[0]) * 1e6, (tr[2] - tr[1]) * 1e6, (tr[3] - tr[2]) * 1e6, (tr[4] - tr[3]) * 1e6,
               (tr[5] - tr[4]) * 1e6, (fh_now() - tr[5]) * 1e6, tr[6], tr[7]);
-    if (g_sigint) sigint_dump(s, n_perm);
+    if (g_sigint) {
+      /* the dump shows every trial up to this one: the bulk results still in flight first
+         (no draws among them) */
+      for (;;) {
+        trial_batch_t *old = NULL;
+        for (k = 0; k < K; k++)
+          if (Bt[k].submitted && (!old || Bt[k].trial < old->trial)) old = &Bt[k];
+        if (!old) break;
+        tb_wait(old, pq);
+        for (k = 0; k < old->n; k++) pq_flush(s, pq, old->pt[k], trial, -1, g, save);
+      }
+      sigint_dump(s, n_perm);
+    }
   }
   /* the bulk batches still in flight, oldest first */
   for (;;) {
@@ -1302,6 +1315,10 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   struct sigaction sa;
   (void)alpha_factor; (void)n_threads; /* -a is inert in the reference too (scan-chromosome.c:584) */
   prepare(s, sm);
+  {
+    const char *e = getenv("FSCL_AMD_SIGINT_WINDOW_MS");
+    g_sigint_window = e ? atof(e) / 1e3 : 10.;
+  }
   memset(&sa, 0, sizeof sa);
   sa.sa_handler = on_sigint;
   sigemptyset(&sa.sa_mask);

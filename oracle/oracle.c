@@ -902,6 +902,39 @@ void orc_free_scan(orc_scan_t *s) {
   free(s->pts); free(s->chr); free(s->snps); free(s->sample_depths); free(s);
 }
 
+static int orc_float_compare(const void *va, const void *vb) { /* scan-chromosome.c:654-658 */
+  const float a = *(const float *)va, b = *(const float *)vb;
+  if (a < b) return -1;
+  if (a > b) return 1;
+  return 0;
+}
+
+/* scan-chromosome.c:753-796: <fname>-nulldist, each point's saved permutation CLRs sorted
+   (the reference writes it from its SIGINT handler, :557-569; here at the end of the run) */
+int orc_output_nulldist(const char *fname, orc_scan_t *s) {
+  char *fn = xmalloc(strlen(fname) + 20);
+  FILE *f;
+  int i, j;
+  sprintf(fn, "%s-nulldist", fname);
+  f = fopen(fn, "w");
+  free(fn);
+  if (!f) return -1;
+  fprintf(f, "chr\tpos\tCLR\talpha\tp\tn");
+  for (j = 0; j < CLR_NULL_DIST_SAVE; j++) fprintf(f, "\t%1.4f", j / (double)CLR_NULL_DIST_SAVE);
+  fprintf(f, "\n");
+  for (i = 0; i < s->n_pts; i++) {
+    orc_pt_t *q = s->pts + i;
+    const int np = CLR_NULL_DIST_SAVE < q->permute_n ? CLR_NULL_DIST_SAVE : q->permute_n;
+    if (q->permute_clr) qsort(q->permute_clr, np, sizeof(float), orc_float_compare);
+    fprintf(f, "%s\t%d\t%1.3f\t%1.3e\t%d\t%d", s->chr[q->chr].name, q->sweep_pos, q->clr, exp(q->lalpha),
+            q->permute_p, q->permute_n);
+    for (j = 0; j < np && q->permute_clr; j++) fprintf(f, "\t%1.2f", (double)q->permute_clr[j]);
+    fprintf(f, "\n");
+  }
+  fclose(f);
+  return 0;
+}
+
 /* fscl.c:316-337 */
 int orc_run_snpfile(const char *snp_fname, const char *out_fname, const orc_opts_t *o,
                     const char *label, orc_stats_t *st) {
@@ -920,6 +953,7 @@ int orc_run_snpfile(const char *snp_fname, const char *out_fname, const orc_opts
   if (o->n_permute > 0) orc_scan_permute(s, tab, o, st);
   orc_scan_output(out_fname, s, o->max_only, o->n_permute, label);
   if (getenv("ORC_DUMP_POINTS")) orc_dump_points(getenv("ORC_DUMP_POINTS"), s);
+  if (getenv("ORC_NULLDIST")) orc_output_nulldist(out_fname, s);
   free_tables(tab, s->n_depths);
   for (i = 0; i < s->n_depths; i++) free(fsp[i]);
   free(fsp);

@@ -160,6 +160,8 @@ void orc_free_scan(orc_scan_t *s);
 
 /* high-precision dump of every scan point (hex floats), for parity tests */
 int orc_dump_points(const char *fname, const orc_scan_t *s);
+/* scan-chromosome.c:753-796: write <fname>-nulldist (sorts each point's saved CLRs) */
+int orc_output_nulldist(const char *fname, orc_scan_t *s);
 
 /* Optional replacement of orc_search_maxalpha inside the position search:
    ref_harness.c plugs the reference's own compiled search_maxalpha in here

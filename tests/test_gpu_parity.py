@@ -382,3 +382,81 @@ def test_back_to_back_scan_permute_continue_the_stream(built, tmp):
     assert [tuple(r) for r in got[["chr", "sweep_pos", "permute_p", "permute_n", "permute_finished"]].tolist()] == \
         [(p[0], p[1], p[10], p[9], p[11]) for p in want]
     assert [c.hex() for c in got["clr"]] == [p[2].hex() for p in want]
+
+
+def test_sigint_dumps_table_and_null_distribution(built, tmp):
+    """SIGINT during the permutation test (scan-chromosome.c:557-569): the CLI writes the
+    current table and <output>-nulldist (:753-796) and keeps going; an interrupt within the
+    window after the start of the permutations or after a dump aborts (exit 255).  The window
+    is the reference's 10 s, shortened here to 300 ms (FSCL_AMD_SIGINT_WINDOW_MS) so that the
+    dump lands after some hundreds of trials.  The dump shows every trial up to the one it
+    follows, so it equals the oracle's final table and null distribution for that many
+    permutations."""
+    import re
+    import signal
+    import threading
+    import time
+    snp = tmp / "sig.snp"
+    # strong planted sweeps: some points are never pruned, so the run outlasts the test
+    synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=6_000_000, snps_per_chr=6000, n=30, seed=97,
+                                                  sweeps_per_chr=2))
+    out = tmp / "g.txt"
+    env = {k: v for k, v in os.environ.items() if k != "FSCL_AMD_DEVICE"}
+    env["FSCL_AMD_SIGINT_WINDOW_MS"] = "300"  # the dump takes a few ms
+    proc = subprocess.Popen([str(CLI), "-f", str(snp), "-o", str(out), "--coarse-grid-spacing=60000",
+                             "--n-permute=1000000", "--n-gpus=1"], stderr=subprocess.PIPE, env=env)
+    seen = [-1]
+
+    def reader():  # progress lines: "\rScanning snp block permutations... <trial> (...)"
+        buf = b""
+        while True:
+            ch = proc.stderr.read(256)
+            if not ch:
+                return
+            buf = (buf + ch)[-4096:]
+            for m in re.finditer(rb"permutations\.\.\.\s+(\d+) \(", buf):
+                seen[0] = max(seen[0], int(m.group(1)))
+
+    th = threading.Thread(target=reader, daemon=True)
+    th.start()
+    try:
+        t0 = time.time()
+        while seen[0] < 0:
+            assert proc.poll() is None, "the CLI ended before the permutations"
+            assert time.time() - t0 < 300, "no permutation progress"
+            time.sleep(0.005)
+        t1 = time.time()
+        while seen[0] < 60 or time.time() - t1 < 0.6:  # past the window after the start
+            assert proc.poll() is None, "the CLI ended before the interrupt"
+            time.sleep(0.005)
+        at = seen[0]
+        proc.send_signal(signal.SIGINT)
+        t2 = time.time()
+        nd = tmp / "g.txt-nulldist"
+        n_pts = None
+        while True:  # the dump ends with a complete null-distribution file; then the window restarts
+            assert proc.poll() is None, f"the CLI ended after the first interrupt (trial {at}, seen {seen[0]})"
+            assert time.time() - t2 < 60, "no dump"
+            if nd.exists() and out.exists():
+                if n_pts is None:
+                    n_pts = len(out.read_text().splitlines()) or None
+                txt = nd.read_text()
+                if n_pts and txt.endswith("\n") and txt.count("\n") == n_pts + 1:
+                    break
+            time.sleep(0.0005)
+        proc.send_signal(signal.SIGINT)
+        t3 = time.time()
+        rc = proc.wait(timeout=60)
+        assert rc == 255, (f"exit {rc}: first interrupt at trial {at} ({t1 - t0:.2f} s to the first trial, "
+                           f"{t2 - t1:.2f} s more), second {t3 - t2:.3f} s later at trial {seen[0]}")
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+            proc.wait()
+    th.join(timeout=10)
+    rows = [line.split("\t") for line in out.read_text().splitlines()]
+    n_trials = max(int(r[5]) for r in rows)  # unfinished points counted every trial 0..T
+    assert n_trials > 60
+    run_oracle(snp, tmp / "o.txt", ["--coarse-grid-spacing=60000", f"--n-permute={n_trials - 1}", "--nulldist"])
+    assert out.read_text() == (tmp / "o.txt").read_text()
+    assert (tmp / "g.txt-nulldist").read_text() == (tmp / "o.txt-nulldist").read_text()
