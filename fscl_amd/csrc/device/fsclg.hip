@@ -888,7 +888,8 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   }
   if (tid == 0) S.n_ties = 0;
   __syncthreads();
-  PHASE_MARK(0);
+  PHASE_MARK(0);  // FSCLG_PHASE_TIMING slots: 0 bounds + layout, 1 wave 0's segments, 2 the wait for
+                  // the other waves, 3 the members' combine + resolve
   TRACE("  bounds done: nw=%d w0 len=%d nl=%d nr=%d\n", nw, S.w[0].len, S.w[0].nl, S.w[0].nr);
   // layout by wave 0, one lane per walk (nw <= MAXWALK = 32), values in registers
   if (wave == 0) {
@@ -944,7 +945,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
     }
   }
   __syncthreads();
-  PHASE_MARK(1);
+  PHASE_MARK(0);
   TRACE("  layout done: segs=%d\n", S.seg_total);
   // static round-robin of the equal-size segments over the waves; the loop
   // counter lives in an SGPR (a per-lane atomic-dispatch loop here was
@@ -976,8 +977,9 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
     }
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
   }
+  PHASE_MARK(1);
   __syncthreads();
-  PHASE_MARK(2);  // FSCLG_PHASE_TIMING: slot 3 holds the members' combine and the resolve
+  PHASE_MARK(2);
   if constexpr (SPLIT) combine_members(S, P, nw);
   TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk<SEGN>(S, tid);
