@@ -72,10 +72,17 @@ constexpr int LDS_WG = FSCLG_LDS_WG;  // LDS per workgroup (default: two workgro
 #ifndef FSCLG_U
 #define FSCLG_U 2
 #endif
-constexpr int U = FSCLG_U;         // terms per lane per loop trip (independent load chains)
+#ifndef FSCLG_U_SPLIT
+#define FSCLG_U_SPLIT 2
+#endif
+// terms per lane per loop trip (independent load chains): the throughput kernel's register
+// budget allows 2; split cells (latency, few waves per SIMD) may take more per trip
+constexpr int U_MAIN = FSCLG_U, U_SPLIT = FSCLG_U_SPLIT;
+constexpr int U_MAX = U_MAIN > U_SPLIT ? U_MAIN : U_SPLIT;
 constexpr double LOG_AD_MIN = -20.0;  // fscl.h:79
 constexpr double LOG_AD_MAX = 4.0;    // fscl.h:80
-constexpr int PAD = 1024;             // slack after pos/row: a trip may read up to 64*U past a walk's end
+constexpr int PAD = 1024;             // slack after pos/row: a trip may read up to 2*64*U past a walk's end
+static_assert(2 * 64 * U_MAX <= PAD, "look-ahead past the padding");
 constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsigned order = signed order
 
 enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2, PF_SPLIT_TIMEOUT = 4 };
@@ -93,6 +100,8 @@ struct Params {
   const double* la_coarse;     // [n_coarse]
   const double* la_refine;     // [n_coarse + 1][MAXREF]; row n_coarse: around LOG_AD_MAX
   const int32_t* n_refine;     // [n_coarse + 1]
+  const uint32_t* dfail;       // [n_coarse + (n_coarse + 1) * MAXREF]: per alpha, the least |d| with
+                               // logt(|d|) + lalpha > LOG_AD_MAX (logt is nondecreasing in |d|)
   const fsclg_cell_t* cells;
   fsclg_point_t* out;
   unsigned long long* stats;   // 8 counters
@@ -144,6 +153,8 @@ struct Walk {
   int wb;         // LDS coefficient window base for this walk
   double la;
   double xl, xr;  // log(alpha d) at the walk's far ends (the walk's largest x is one of them)
+  uint32_t dfail; // a site is outside the walk iff its |d| >= dfail (Params::dfail)
+  int pad_;
 };
 
 struct Smem {
@@ -177,7 +188,22 @@ struct Smem {
   int inst;                       // split cells: eval_walks instances so far (the XAcc region in turn)
   int xbase;                      // split cells: this member's first tie slot
   int xfail;                      // split cells: PF_SPLIT_TIMEOUT if a member never arrived
+  int iev;                        // FSCLG_INST_TRACE: events recorded so far
 };
+
+// FSCLG_INST_TRACE (development aid): thread 0 of cell 0's first member records timestamped
+// events (tag, a, b) after the per-cell trace area: [count, then 4 words per event]
+#ifdef FSCLG_INST_TRACE
+#define IEV(tag, a, b) do { \
+    if (P.ctrace && S.cell == 0 && S.member == 0 && threadIdx.x == 0 && S.iev < 4000) { \
+      unsigned long long* q_ = P.ctrace + 8 * (size_t)P.n_cells; \
+      const int k_ = S.iev++; \
+      q_[1 + 4 * k_] = wall_clock64(); q_[2 + 4 * k_] = (tag); q_[3 + 4 * k_] = (unsigned long long)(a); \
+      q_[4 + 4 * k_] = (unsigned long long)(b); q_[0] = (unsigned long long)S.iev; \
+    } } while (0)
+#else
+#define IEV(tag, a, b) do { } while (0)
+#endif
 
 // a split cell's shared per-instance accumulator: integer sums add in any order (exact), the
 // segments' parity bits XOR (each segment has one member), the fp64 sums of lanes past 2^51 stay
@@ -290,7 +316,7 @@ __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, co
 
 // coefficients of U terms: the intervals of all U first (their threshold reads overlap),
 // then per term the LDS window or, for lanes outside it, the global table
-template <bool LDS>
+template <bool LDS, int U>
 __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t (&rv)[U], const Smem& S,
                                            const Params& P, int ivc0, double2 (&ca)[U], double2 (&cb)[U],
                                            int (&iv)[U]) {
@@ -351,7 +377,7 @@ __device__ __forceinline__ int group_search(int lo, int hi, int lane, F pred) {
     if (act) t = pred(lo + 1 + (int)((span * j) / G));
     const unsigned long long b = __ballot(t);
     if (act) {
-      const unsigned long long gm = G == 64 ? b : ((b >> sh) & ((1ull << G) - 1));
+      const unsigned long long gm = G == 64 ? b : ((b >> sh) & ((1ull << (G & 63)) - 1));
       const int c = __popcll(gm);  // the probes are nondecreasing: T holds on the first c
       const int nlo = c > 0 ? lo + 1 + (int)((span * (c - 1)) / G) : lo;
       const int nhi = c < G ? lo + 1 + (int)((span * c) / G) : hi;
@@ -404,32 +430,38 @@ __device__ __forceinline__ void set_binade(Pt& pt) {
   pt.inv_u = __longlong_as_double((long long)(1023 + 52 - e) << 52);
 }
 
-// walk_bounds for every walk side of the phase: 8 lanes per (walk, side), a 9-way search
-// of the same monotone predicates (left: log(alpha d) > 4 holds on a prefix of
-// (wstart - 1, near); right, when the first right neighbour is inside: its negation holds on
-// a prefix of (near + 1, wend + 1))
-__device__ __forceinline__ void walk_bounds_par(Smem& S, const Params& P, int tid, int nw) {
-  const int lane = tid & 63, g = tid >> 3;
+// walk_bounds for every walk side of the phase: G lanes per (walk, side), a (G+1)-way search
+// of the same monotone predicates as sm-search.c:112-147's loops (left: the site is outside,
+// log(alpha d) > 4, on a prefix of (wstart - 1, near); right, when the first right neighbour
+// is inside: inside on a prefix of (near + 1, wend + 1)).  logt is nondecreasing in |d|, so
+// log(alpha d) > 4 is |d| >= dfail, an integer compare per probe (no log-table gather in the
+// search's dependent rounds; the host derives dfail from the same table and adds).
+template <int G>
+__device__ __forceinline__ void walk_bounds_g(Smem& S, const Params& P, int tid, int nw) {
+  const int lane = tid & 63, g = tid / G;
   const bool act = g < 2 * nw;
   const int w = act ? g >> 1 : 0, side = g & 1;
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[act ? W.p : 0];
-  const int near = pt.nearest, sweep = pt.sweep;
-  const double la = W.la;
+  const int near = pt.nearest;
+  const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS, df = W.dfail;
+  auto outside = [&](int i) { return absdist(P.pr[i].x, usweep) >= df; };
   int lo = 0, hi = 1;
   bool ok1 = false;
   if (act) {
     if (side == 0) { lo = pt.wstart - 1; hi = near; }
     else {
-      ok1 = near + 1 <= pt.wend && !(log_ad_of(near + 1, sweep, la, P) > LOG_AD_MAX);
+      ok1 = near + 1 <= pt.wend && !outside(near + 1);
       if (ok1) { lo = near + 1; hi = pt.wend + 1; }
     }
   }
-  const int e = group_search<8>(lo, hi, lane, [&](int m) { return (log_ad_of(m, sweep, la, P) > LOG_AD_MAX) != (side == 1); });
-  if (act && (tid & 7) == 0) {
+  const int e = group_search<G>(lo, hi, lane, [&](int m) { return outside(m) != (side == 1); });
+  if (act && (tid & (G - 1)) == 0) {
     Walk& V = S.w[w];
+    const int sweep = pt.sweep;
+    const double la = W.la;
     if (side == 0) {
-      V.len = log_ad_of(near, sweep, la, P) > LOG_AD_MAX ? 0 : 1;
+      V.len = outside(near) ? 0 : 1;
       V.nl = near - e;
       V.xl = log_ad_of(e < near ? e : near, sweep, la, P);
     } else {
@@ -438,6 +470,11 @@ __device__ __forceinline__ void walk_bounds_par(Smem& S, const Params& P, int ti
       V.xr = log_ad_of(r, sweep, la, P);
     }
   }
+}
+
+__device__ __forceinline__ void walk_bounds_par(Smem& S, const Params& P, int tid, int nw) {
+  if (2 * nw * 16 <= WG) walk_bounds_g<16>(S, P, tid, nw);  // uniform over the workgroup
+  else walk_bounds_g<8>(S, P, tid, nw);
 }
 
 // exact sequential sum of one walk by one wave (slow path, settles an argmax), 64 terms at
@@ -524,7 +561,7 @@ __device__ __forceinline__ double uniform_f64(double v) {
 // window or the global table, a uniform branch).  Otherwise the trip takes the per-lane path
 // of run_segment and re-centres civ on its last site.  Only the final trip of a segment
 // masks lanes past its end (zero sentinel row).
-template <bool LDS, int SEGN>
+template <bool LDS, int SEGN, int U>
 __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Params& P, int lane, double& acc,
                                                 double& accm) {
   const Walk& W = S.w[w];
@@ -611,7 +648,7 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
       }
     } else {
       int iv[U];
-      coef_stage<LDS>(x, rv, S, P, ivc0, ca, cb, iv);
+      coef_stage<LDS, U>(x, rv, S, P, ivc0, ca, cb, iv);
       civ = __builtin_amdgcn_readlane(iv[U - 1], 63);  // the trip's last site
     }
     double nul[U];
@@ -821,7 +858,9 @@ __device__ __forceinline__ void combine_members(Smem& S, const Params& P, int nw
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
+#ifndef FSCLG_XP_NO_REL
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned int* cnt = P.xcnt + S.cell;
     ag_add32(cnt, 1u);
@@ -831,7 +870,9 @@ __device__ __forceinline__ void combine_members(Smem& S, const Params& P, int nw
       __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > 100000000ull) { S.xfail = PF_SPLIT_TIMEOUT; break; }  // ~1 s at 100 MHz
     }
+#ifndef FSCLG_XP_NO_ACQ
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
@@ -888,6 +929,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   }
   if (tid == 0) S.n_ties = 0;
   __syncthreads();
+  IEV(1, nw, 0);  // bounds done
   PHASE_MARK(0);  // FSCLG_PHASE_TIMING slots: 0 bounds + layout, 1 wave 0's segments, 2 the wait for
                   // the other waves, 3 the members' combine + resolve
   TRACE("  bounds done: nw=%d w0 len=%d nl=%d nr=%d\n", nw, S.w[0].len, S.w[0].nl, S.w[0].nr);
@@ -914,7 +956,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
     // walks in descending window base, stable: each walk's rank and first segment
     int rank = 0, seg0 = 0;
     for (int j = 0; j < nw; j++) {
-      const int wbj = __shfl(wb, j, 64), nsj = __shfl(nseg, j, 64);
+      const int wbj = __builtin_amdgcn_readlane(wb, j), nsj = __builtin_amdgcn_readlane(nseg, j);  // j uniform
       const bool before = wbj > wb || (wbj == wb && j < lane);
       rank += before ? 1 : 0;
       seg0 += before ? nsj : 0;
@@ -925,7 +967,8 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
     int ng = 0, gprev = 0;
     for (int k = 0; k < nw; k++) {
       const int l = __ffsll((unsigned long long)__ballot(act && rank == k)) - 1;
-      const int wbk = __shfl(wb, l, 64), lenk = __shfl(len, l, 64), s0k = __shfl(seg0, l, 64);
+      const int wbk = __builtin_amdgcn_readlane(wb, l), lenk = __builtin_amdgcn_readlane(len, l),
+                s0k = __builtin_amdgcn_readlane(seg0, l);
       if (lenk && (ng == 0 || wbk < gprev - 2)) {
         if (lane == 0) { S.gwb[ng] = wbk; S.gseg[ng] = s0k; }
         ng++;
@@ -945,6 +988,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
     }
   }
   __syncthreads();
+  IEV(2, S.seg_total, S.ngrp);  // layout done
   PHASE_MARK(0);
   TRACE("  layout done: segs=%d\n", S.seg_total);
   // static round-robin of the equal-size segments over the waves; the loop
@@ -952,7 +996,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   // miscompiled into a loop that never re-issued its atomic)
   {
     const int ngrp = __builtin_amdgcn_readfirstlane(S.ngrp);
-    int k = 0, cw = -1;
+    int k = 0, cw = -1, nsg = 0;
     double acc = 0.0, accm = 0.0;
     for (int gi = 0; gi < ngrp; gi++) {
      const int gwb = __builtin_amdgcn_readfirstlane(S.gwb[gi]);
@@ -972,19 +1016,24 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
         if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
         cw = w; acc = 0.0; accm = 0.0;
       }
-      run_segment_idx<LDS, SEGN>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+      run_segment_idx<LDS, SEGN, SPLIT ? U_SPLIT : U_MAIN>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
+      nsg++;
      }
     }
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
+    IEV(3, nsg, 0);  // wave 0's segments done
   }
   PHASE_MARK(1);
   __syncthreads();
+  IEV(4, 0, 0);  // every wave's segments done
   PHASE_MARK(2);
   if constexpr (SPLIT) combine_members(S, P, nw);
+  IEV(5, 0, 0);  // combined
   TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk<SEGN>(S, tid);
   if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;
   __syncthreads();
+  IEV(6, 0, 0);  // resolved
   PHASE_MARK(3);
 #undef PHASE_MARK
   TRACE("eval_walks: nw=%d segs=%d ties=%d\n", nw, S.seg_total, S.n_ties);
@@ -1018,12 +1067,14 @@ template <bool LDS, bool SPLIT = false>
 __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < np) set_binade(S.pt[p0 + tid]);
+  IEV(0, np, S.pt[p0].sweep);  // an alpha search starts
   TRACE("maxalpha: p0=%d np=%d sweep=%d N=%g\n", p0, np, S.pt[p0].sweep, S.pt[p0].N);
   // ---- coarse phase
   if (tid < np * P.n_coarse) {
     const int p = tid / P.n_coarse, a = tid % P.n_coarse;
     S.w[tid].p = p0 + p;
     S.w[tid].la = P.la_coarse[a];
+    S.w[tid].dfail = P.dfail[a];
     S.w[tid].len = 0; S.w[tid].nl = S.w[tid].nr = 0;
   }
   if (tid == 0) { S.nwalk = np * P.n_coarse; S.cnt[3] += np; S.hkey = 0; }
@@ -1073,6 +1124,7 @@ __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, in
           for (int r = 0; r < cnt; r++, nw++) {
             S.w[nw].p = p0 + p;
             S.w[nw].la = P.la_refine[ci * MAXREF + r];
+            S.w[nw].dfail = P.dfail[P.n_coarse + ci * MAXREF + r];
             S.w[nw].len = 0; S.w[nw].nl = S.w[nw].nr = 0;
           }
         }
@@ -1107,13 +1159,7 @@ __device__ __forceinline__ void write_point(fsclg_point_t& o, const Pt& pt) {
 }
 
 template <bool LDS, bool SPLIT>
-#ifdef FSCLG_WPE  // waves per SIMD to budget registers for (caps VGPRs at 512 / FSCLG_WPE)
-#define FSCLG_KATTR __attribute__((amdgpu_waves_per_eu(FSCLG_WPE, FSCLG_WPE)))
-#else
-#define FSCLG_KATTR
-#endif
-__global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P) {
-  __shared__ Smem S;
+__device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // cells arrive in the host's longest-first order (XCD-aware: blocks b and b + 8 share an
   // XCD); the hardware dispatches blocks in order (round-robin over the XCDs), so the long
@@ -1129,7 +1175,7 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
   }
   if (tid < 8) S.cnt[tid] = 0;
   if (tid < 4) S.tph[tid] = 0;
-  if (tid == 0) { S.cell = cell; S.member = member; S.inst = 0; S.xfail = 0; }
+  if (tid == 0) { S.cell = cell; S.member = member; S.inst = 0; S.xfail = 0; S.iev = 0; }
   if (P.ctrace && tid == 0 && member == 0) { P.ctrace[8 * cell] = wall_clock64(); P.ctrace[8 * cell + 2] = __smid(); }
   if constexpr (LDS) {
     double* thr = reinterpret_cast<double*>(fsclg_dyn + P.off_thr);
@@ -1206,6 +1252,26 @@ __global__ void __launch_bounds__(WG) FSCLG_KATTR search_maxpos_kernel(Params P)
     P.ctrace[8 * cell + 1] = wall_clock64(); P.ctrace[8 * cell + 3] = S.cnt[0];
     for (int k = 0; k < 4; k++) P.ctrace[8 * cell + 4 + k] = S.tph[k];
   }
+}
+
+// waves per SIMD to budget registers for (caps VGPRs at 512 / waves): the throughput kernel
+// runs two workgroups per CU (6 waves per SIMD); a split launch (few cells, latency) keeps
+// its workgroups far apart and may spend more registers per wave on wider trips
+#ifndef FSCLG_WPE_SPLIT
+#define FSCLG_WPE_SPLIT 6
+#endif
+template <bool LDS>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(FSCLG_WPE, FSCLG_WPE)))
+search_maxpos_kernel(Params P) {
+  __shared__ Smem S;
+  maxpos_body<LDS, false>(S, P);
+}
+
+template <bool LDS>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(FSCLG_WPE_SPLIT, FSCLG_WPE_SPLIT)))
+search_maxpos_split_kernel(Params P) {
+  __shared__ Smem S;
+  maxpos_body<LDS, true>(S, P);
 }
 
 // ------------------------------------------------------------ window null sums
@@ -1326,6 +1392,7 @@ struct Batch {
   int ept_cap = 0, pep_cap = 0, pcep_cap = 0;
   unsigned long long* p_ctrace = nullptr;  // FSCLG_CELL_TRACE=<file>: per-cell timing appended per launch
   int ctrace_cap = 0;
+  int trace_n = 0;                  // cells of the traced launch (the event area follows them)
   unsigned long long* ivhist = nullptr;    // this launch measures the interval histogram (FSCLG_IVHIST)
   bool traced = false;
   std::unordered_map<unsigned long long, int> umap, emap;
@@ -1382,6 +1449,7 @@ struct fsclg_ctx {
   // alpha grid
   std::vector<double> h_coarse, h_refine;
   std::vector<int32_t> h_nref;
+  uint32_t* d_dfail = nullptr;     // walk thresholds of the alpha grid (Params::dfail)
   double* d_la_coarse = nullptr;
   double* d_la_refine = nullptr;
   int32_t* d_n_refine = nullptr;
@@ -1415,6 +1483,8 @@ static int upload(T** dst, const T* src, size_t n, hipStream_t s) {
   }
   return FSCLG_OK;
 }
+
+static int update_dfail(fsclg_ctx* c);
 
 // least double x with (int)((x - LOG_AD_MIN) / step) >= j (sm-spline.c:52), by bisection over the
 // ordered doubles; the host evaluates the reference's expression with IEEE division
@@ -1498,7 +1568,7 @@ int fsclg_close(fsclg_ctx* c) {
   hipDeviceSynchronize();
   void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0,
                   c->d_chr_start, c->d_chr_n, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine,
-                  c->d_stats};
+                  c->d_stats, c->d_dfail};
   for (void* p : ptrs) if (p) hipFree(p);
   for (Slot& S : c->slot) {
     for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null}) if (p) hipFree(p);
@@ -1550,6 +1620,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
     }
   if ((r = upload(&c->d_logt, lt3.data(), lt3.size(), c->ustream))) return r;
   c->h_lt3.swap(lt3);
+  if ((r = update_dfail(c))) return r;
   // [row][iv][4] -> [iv][plane][1 + row][2] (coef_off): device row 0 is an all-zero sentinel
   // (terms exactly 0); plane 0 holds (c0, c1), plane 1 (c2, c3)
   const size_t stride = (size_t)n_rows + 1;
@@ -1763,7 +1834,40 @@ int fsclg_set_alpha_grid(fsclg_ctx* c, const double* coarse, int n_coarse, const
   c->h_refine.assign(refine, refine + (size_t)(n_coarse + 1) * MAXREF);
   c->h_nref.assign(n_refine, n_refine + n_coarse + 1);
   c->plan_dirty = true;
-  return FSCLG_OK;
+  return update_dfail(c);
+}
+
+// Params::dfail for every alpha of the grid, once both the log table and the grid are set:
+// logt3 as a function of |d| (sm-search.c:40-46) is nondecreasing (checked), so the sites of a
+// walk are those with logt(|d|) + lalpha <= LOG_AD_MAX, i.e. |d| < dfail
+static int update_dfail(fsclg_ctx* c) {
+  if (c->h_lt3.empty() || c->h_coarse.empty()) return FSCLG_OK;
+  const std::vector<double>& T = c->h_lt3;
+  auto lt = [&](uint64_t ad) {
+    const uint32_t sh = ad > 0xFFFFFFu ? 16u : (ad > 0xFFFFu ? 8u : 0u);
+    return T[(size_t)(ad >> sh) + ((size_t)sh << 13)];
+  };
+  for (int b = 0; b < 3; b++)  // monotone within each branch's used entries and across branches
+    for (int i = (b ? 257 : 1); i < 0x10000; i++)
+      if (!(T[(size_t)b * 0x10000 + i - 1] <= T[(size_t)b * 0x10000 + i]))
+        return set_err(FSCLG_E_ARG, "log table not monotone");
+  if (!(T[0xFFFF] <= T[0x10000 + 256]) || !(T[0x1FFFF] <= T[0x20000 + 256]))
+    return set_err(FSCLG_E_ARG, "log table not monotone across branches");
+  std::vector<double> las(c->h_coarse);
+  las.insert(las.end(), c->h_refine.begin(), c->h_refine.end());
+  std::vector<uint32_t> df(las.size());
+  for (size_t k = 0; k < las.size(); k++) {
+    const double la = las[k];
+    auto fails = [&](uint64_t d) { volatile double x = lt(d) + la; return x > LOG_AD_MAX; };
+    uint64_t lo = 0, hi = 0xFFFFFFFFull;  // the least failing d in [lo, hi], hi if none below it
+    if (!fails(hi)) { df[k] = 0xFFFFFFFFu; continue; }
+    while (lo < hi) {
+      const uint64_t m = lo + (hi - lo) / 2;
+      if (fails(m)) hi = m; else lo = m + 1;
+    }
+    df[k] = (uint32_t)lo;
+  }
+  return upload(&c->d_dfail, df.data(), df.size(), c->ustream);
 }
 
 static int ensure_io(Batch& B, int n) {
@@ -1915,6 +2019,7 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.lt_span = c->lt_hi > 256 ? ((uint32_t)c->lt_hi << 16) - 0x1000000u : 0u;  // lt_hi <= 32768
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = S.d_chr_null; P.win_null = S.d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
+  P.dfail = c->d_dfail;
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
   P.split = 1; P.xacc = nullptr; P.xcnt = nullptr;
@@ -1922,7 +2027,8 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
     if (B.ctrace_cap < n) {
       if (B.p_ctrace) hipHostFree(B.p_ctrace);
       B.p_ctrace = nullptr; B.ctrace_cap = 0;
-      if (hipHostMalloc((void**)&B.p_ctrace, sizeof(unsigned long long) * 8 * n, HOSTMEM) == hipSuccess) B.ctrace_cap = n;
+      if (hipHostMalloc((void**)&B.p_ctrace, sizeof(unsigned long long) * (8 * (size_t)n + 16008), HOSTMEM) == hipSuccess)
+        B.ctrace_cap = n;  // + the FSCLG_INST_TRACE event area
     }
     P.ctrace = B.p_ctrace;
   }
@@ -1941,17 +2047,17 @@ static int launch_blocks(hipStream_t stream, const Params& P, int n) {
     int dev = 0;
     HIPCHK(hipGetDevice(&dev), "hipGetDevice");
     if (dev >= 64 || !(attr_set >> dev & 1ull)) {
-      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true, false>),
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
-      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true, true>),
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_split_kernel<true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
       if (dev < 64) attr_set |= 1ull << dev;
     }
-    if (P.split > 1) hipLaunchKernelGGL((search_maxpos_kernel<true, true>), dim3(grid), dim3(WG), dyn, stream, P);
-    else hipLaunchKernelGGL((search_maxpos_kernel<true, false>), dim3(grid), dim3(WG), dyn, stream, P);
+    if (P.split > 1) hipLaunchKernelGGL((search_maxpos_split_kernel<true>), dim3(grid), dim3(WG), dyn, stream, P);
+    else hipLaunchKernelGGL((search_maxpos_kernel<true>), dim3(grid), dim3(WG), dyn, stream, P);
   } else
-    if (P.split > 1) hipLaunchKernelGGL((search_maxpos_kernel<false, true>), dim3(grid), dim3(WG), 0, stream, P);
-    else hipLaunchKernelGGL((search_maxpos_kernel<false, false>), dim3(grid), dim3(WG), 0, stream, P);
+    if (P.split > 1) hipLaunchKernelGGL((search_maxpos_split_kernel<false>), dim3(grid), dim3(WG), 0, stream, P);
+    else hipLaunchKernelGGL((search_maxpos_kernel<false>), dim3(grid), dim3(WG), 0, stream, P);
   HIPCHK(hipGetLastError(), "launch search_maxpos_kernel");
   return FSCLG_OK;
 }
@@ -2186,6 +2292,7 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
   HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
   HIPCHK(hipEventRecord(B.ev2, B.stream), "hipEventRecord");
   B.traced = P.ctrace != nullptr;
+  B.trace_n = nl;
   B.nu = nl;
   B.nlaunch = use_ep ? 2 : 1;
   B.pending = true;
@@ -2224,6 +2331,14 @@ int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
   if (B.traced) {  // development aid: append [n, then n x (start, end, cu, terms, 4 phase times)] to the file
     std::vector<unsigned long long> h((size_t)8 * nu);
     memcpy(h.data(), B.p_ctrace, sizeof(unsigned long long) * h.size());
+    if (const char* ie = getenv("FSCLG_INST_TRACE_FILE")) {  // cell 0's events: [count, 4 x count]
+      const unsigned long long* q = B.p_ctrace + 8 * (size_t)B.trace_n;
+      if (FILE* f = fopen(ie, "ab")) {
+        fwrite(q, sizeof(unsigned long long), 1 + 4 * (size_t)std::min(q[0], 4000ull), f);
+        fclose(f);
+      }
+      memset(B.p_ctrace + 8 * (size_t)B.trace_n, 0, sizeof(unsigned long long) * 16008);
+    }
     if (FILE* f = fopen(getenv("FSCLG_CELL_TRACE"), "ab")) {
       const unsigned long long nn = (unsigned long long)nu;
       fwrite(&nn, sizeof nn, 1, f);
