@@ -735,9 +735,17 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
   const bool safe = !big && !overflow && S0 < 0 && (S0 + Qn - T >= LO) && (S0 + Pp + T <= HI);
   if (safe) {
     const int nl = W.nl, nsl = W.nsl;
-    auto segbit = [&](int sg) { return (int)(S.segbits[w][sg >> 5] >> (sg & 31)) & 1; };
-    int lpar = 0;
-    for (int sg = 0; sg < nsl; sg++) lpar ^= segbit(sg);
+    auto segpar = [&](int a, int b) {  // parity of the segment bits [a, b)
+      int par = 0;
+      for (int j = a >> 5; j <= (b - 1) >> 5 && a < b; j++) {
+        unsigned int m = S.segbits[w][j];
+        if (j == a >> 5) m &= ~0u << (a & 31);
+        if (j == (b - 1) >> 5 && (b & 31)) m &= ~0u >> (32 - (b & 31));
+        par ^= __popc(m) & 1;
+      }
+      return par;
+    };
+    const int lpar = segpar(0, nsl);
     int adjx = 0;
     long long adjs = 0;
     int prevk = -1;
@@ -755,8 +763,7 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
       // right part before it; R of a tie is even, so both read lpar ^ prefix-in-part
       const int jj = bestv & 0x3FFFF;
       const int sg = seg_of<SEGN>(W, pt, pt.nearest - nl + jj);
-      int sp = 0;
-      for (int t = (jj <= nl ? 0 : nsl); t < sg; t++) sp ^= segbit(t);
+      const int sp = segpar(jj <= nl ? 0 : nsl, sg);
       const int pre = (bestv >> 18) & 1, up = (bestv >> 19) & 1;
       const int adj = (int)(S0 & 1) ^ lpar ^ sp ^ pre ^ adjx;
       adjx ^= adj;
@@ -1062,6 +1069,36 @@ __device__ __forceinline__ int argmax_or_mark(Smem& S, int first, int count, dou
   return amb ? AMBIG : bi;
 }
 
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// argmax_or_mark by one wave, lane c holding candidate first + c (count <= 64): the sequential
+// loop's winner is the first exact candidate holding the largest exact value above the prior
+// (strict '>': a later equal value never replaces it; NaN never wins); the best lower bound and
+// the marks as there.  Every lane returns the result.
+__device__ __forceinline__ int argmax_wave(Smem& S, int first, int count, double prior_val, int lane) {
+  const bool in = lane < count;
+  const int c = first + (in ? lane : 0);
+  const bool ex = in && S.exact[c] != 0;
+  const double v = S.val[c], a = S.appr[c], b = S.bnd[c];
+  const bool cand = ex && v > prior_val;
+  const unsigned long long cm = __ballot(cand);
+  int bi = PRIOR;
+  double bv = prior_val;
+  if (cm) {
+    bv = wave_max_f64(cand ? v : -__builtin_inf());
+    bi = first + __ffsll(__ballot(cand && v == bv)) - 1;
+  }
+  const bool inx = in && !ex;
+  const double lb = fmax(bv, wave_max_f64(inx ? a - b : -__builtin_inf()));  // NaN bounds ignored, as '>' does
+  const bool mark = inx && !(a + b < lb);
+  if (mark) S.need_slow[c] = 1;
+  return __ballot(mark) ? AMBIG : bi;
+}
+
 // search_maxalpha for the points in slots [p0, p0+np) (sm-search.c:269-300)
 template <bool LDS, bool SPLIT = false>
 __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
@@ -1083,18 +1120,19 @@ __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, in
     eval_walks<LDS, SPLIT>(S, P);
     // argmax per point, with slow-path settling
     for (int round = 0; round < 2; round++) {
-      if (tid == 0) {
-        S.n_slow = 0;
+      if (wave == 0) {
+        int slow = 0;
         for (int p = 0; p < np; p++) {
           const Pt& pt = S.pt[p0 + p];
           int first, count;
           double pv;
           if (phase == 0) { first = p * P.n_coarse; count = P.n_coarse; pv = -1.7976931348623157e308; }
           else { first = pt.pad >> 8; count = pt.pad & 0xFF; pv = pt.sm; }
-          const int r = argmax_or_mark(S, first, count, pv);
-          if (r == AMBIG) S.n_slow = 1;
-          S.best[p] = r;
+          const int r = argmax_wave(S, first, count, pv, lane);
+          if (r == AMBIG) slow = 1;
+          if (lane == 0) S.best[p] = r;
         }
+        if (lane == 0) S.n_slow = slow;
       }
       __syncthreads();
       if (S.n_slow == 0) break;
@@ -1109,36 +1147,43 @@ __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, in
       __syncthreads();
     }
     if (phase == 0) {
-      // record coarse winners (or the untouched initial state), lay out refine walks
-      if (tid == 0) {
-        int nw = 0;
-        for (int p = 0; p < np; p++) {
-          const int bi = S.best[p];
-          Pt& pt = S.pt[p0 + p];
-          int ci;
+      // record coarse winners (or the untouched initial state), lay out refine walks: wave 0,
+      // lane p for point p, then lane p * MAXREF + r for its refine walk r
+      if (wave == 0) {
+        int ci = 0, cnt = 0;
+        if (lane < np) {
+          const int bi = S.best[lane];
+          Pt& pt = S.pt[p0 + lane];
           if (bi == PRIOR) { pt.la = LOG_AD_MAX; pt.sm = -1.7976931348623157e308; ci = P.n_coarse; }
-          else { pt.la = S.w[bi].la; pt.sm = S.val[bi]; ci = bi - p * P.n_coarse; }
-          const int cnt = P.n_refine[ci];
-          pt.pad = (nw << 8) | cnt;
-          if (p == 0) S.hkey = 1 + ci;
-          for (int r = 0; r < cnt; r++, nw++) {
-            S.w[nw].p = p0 + p;
-            S.w[nw].la = P.la_refine[ci * MAXREF + r];
-            S.w[nw].dfail = P.dfail[P.n_coarse + ci * MAXREF + r];
-            S.w[nw].len = 0; S.w[nw].nl = S.w[nw].nr = 0;
-          }
+          else { pt.la = S.w[bi].la; pt.sm = S.val[bi]; ci = bi - lane * P.n_coarse; }
+          cnt = P.n_refine[ci];
         }
-        S.nwalk = nw;
+        int off = 0, nw = 0;
+        for (int p = 0; p < np; p++) {  // np <= 3, uniform
+          const int cp = __builtin_amdgcn_readlane(cnt, p);
+          if (lane == p) off = nw;
+          nw += cp;
+        }
+        if (lane < np) S.pt[p0 + lane].pad = (off << 8) | cnt;
+        if (lane == 0) { S.hkey = 1 + ci; S.nwalk = nw; }
+        const int p = lane / MAXREF, r = lane % MAXREF;
+        const int pc = p < np ? p : 0;
+        const int cip = __shfl(ci, pc, 64), cntp = __shfl(cnt, pc, 64), offp = __shfl(off, pc, 64);
+        if (p < np && r < cntp) {
+          Walk& V = S.w[offp + r];
+          V.p = p0 + p;
+          V.la = P.la_refine[cip * MAXREF + r];
+          V.dfail = P.dfail[P.n_coarse + cip * MAXREF + r];
+          V.len = 0; V.nl = V.nr = 0;
+        }
       }
       __syncthreads();
     } else {
-      if (tid == 0) {
-        for (int p = 0; p < np; p++) {
-          Pt& pt = S.pt[p0 + p];
-          const int bi = S.best[p];
-          if (bi != PRIOR) { pt.la = S.w[bi].la; pt.sm = S.val[bi]; }
-          pt.clr = 2.0 * (pt.sm - pt.N);  // sm-search.c:298
-        }
+      if (tid < np) {
+        Pt& pt = S.pt[p0 + tid];
+        const int bi = S.best[tid];
+        if (bi != PRIOR) { pt.la = S.w[bi].la; pt.sm = S.val[bi]; }
+        pt.clr = 2.0 * (pt.sm - pt.N);  // sm-search.c:298
       }
       __syncthreads();
     }
