@@ -83,6 +83,7 @@ constexpr double LOG_AD_MIN = -20.0;  // fscl.h:79
 constexpr double LOG_AD_MAX = 4.0;    // fscl.h:80
 constexpr int PAD = 1024;             // slack after pos/row: a trip may read up to 2*64*U past a walk's end
 static_assert(2 * 64 * U_MAX <= PAD, "look-ahead past the padding");
+static_assert(SEG_SPLIT % (64 * U_SPLIT) == 0 && SEG % (64 * U_MAIN) == 0, "segments of whole trips");
 constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsigned order = signed order
 
 enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2, PF_SPLIT_TIMEOUT = 4 };
@@ -131,10 +132,10 @@ struct Params {
   fsclg_point_t* ept;          // mode 2 out / mode 0 in: evaluated endpoints
   const int2* cell_ep;         // mode 0: (start, end) endpoint indices of each cell, or null
   // split cells (mode 0): `split` workgroups ("members") per cell share every walk's segments and
-  // combine their partial sums through a per-cell accumulator in global memory (XAcc, three
-  // regions used in turn, zeroed before the launch) and a per-cell arrival counter
+  // combine their partial sums through a per-cell exchange area in global memory (XAcc, two
+  // regions used in turn) and a per-cell arrival counter (zeroed before the launch)
   int split;                   // members per cell (1: one workgroup per cell)
-  char* xacc;                  // [n_cells][3] XAcc
+  char* xacc;                  // [n_cells][2] XAcc
   unsigned int* xcnt;          // [n_cells] arrivals
 };
 
@@ -189,6 +190,7 @@ struct Smem {
   int xbase;                      // split cells: this member's first tie slot
   int xfail;                      // split cells: PF_SPLIT_TIMEOUT if a member never arrived
   int iev;                        // FSCLG_INST_TRACE: events recorded so far
+  int xnt[8];                     // split cells: each member's tie count of the instance
 };
 
 // FSCLG_INST_TRACE (development aid): thread 0 of cell 0's first member records timestamped
@@ -205,18 +207,21 @@ struct Smem {
 #define IEV(tag, a, b) do { } while (0)
 #endif
 
-// a split cell's shared per-instance accumulator: integer sums add in any order (exact), the
-// segments' parity bits XOR (each segment has one member), the fp64 sums of lanes past 2^51 stay
-// per member and are added in member order (every member reads the same value)
+// a split cell's exchange area for one instance: every member writes its own slots with plain
+// stores (no zeroing, no read-modify-write); after the arrival counter every member reads all
+// members' slots and combines them the same way -- integer sums in any order (exact), the
+// segments' parity bits by XOR (each segment has one member), the fp64 sums of lanes past 2^51
+// in member order, the ties concatenated.  Two areas used in turn: a member writes instance
+// i + 2 only after every member has arrived at i + 1, i.e. has finished reading i.
 constexpr int MAXSPLIT = 8;
+constexpr int XTIES = MAXTIES / MAXSPLIT;  // tie slots per member (more: the overflow path)
 struct XAcc {
-  unsigned long long P[MAXWALK], Q[MAXWALK];
+  unsigned long long P[MAXSPLIT][MAXWALK], Q[MAXSPLIT][MAXWALK];
   double Pd[MAXSPLIT][MAXWALK], Qd[MAXSPLIT][MAXWALK];
-  unsigned int wflag[MAXWALK];
-  unsigned int segbits[MAXWALK][SEGWORDS];
-  unsigned int n_ties;
-  unsigned int pad;
-  int ties[MAXTIES];
+  unsigned int wflag[MAXSPLIT][MAXWALK];
+  unsigned int segbits[MAXSPLIT][MAXWALK][SEGWORDS];
+  unsigned int nt[MAXSPLIT];
+  int ties[MAXSPLIT][XTIES];
 };
 
 // dynamic LDS of a workgroup (LDS = true): coefficient planes of the top K intervals, the
@@ -562,8 +567,8 @@ __device__ __forceinline__ double uniform_f64(double v) {
 // of run_segment and re-centres civ on its last site.  Only the final trip of a segment
 // masks lanes past its end (zero sentinel row).
 template <bool LDS, int SEGN, int U>
-__device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Params& P, int lane, double& acc,
-                                                double& accm) {
+__device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, const Params& P, int lane,
+                                                double& acc, double& accm) {
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[W.p];
   const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS;
@@ -571,14 +576,15 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
   const int lo = pt.nearest - W.nl;
   int ib, ie;
   seg_bounds<SEGN>(W, pt, s, ib, ie);
-  const int n = ie - ib;
+  int n = ie - ib;
   const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
   const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
   int civ = 0;
   double sum = 0.0, mag = 0.0;
   // the sites of the next trip are loaded one trip ahead (nx), issued after the trip's own
   // coefficient loads so that waiting for a global coefficient gather (vmcnt counts in
-  // order) does not wait for them; PAD covers the look-ahead past a segment's end
+  // order) does not wait for them; PAD covers the look-ahead past a segment's end.  Segments
+  // [s, s1) of one part are contiguous: the look-ahead runs on into the next one
   uint2 nx[U];
 #pragma unroll
   for (int u = 0; u < U; u++) nx[u] = ld_pr(P.pr, (uint32_t)(ib + 64 * u + lane));
@@ -682,13 +688,21 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, const Par
       mag += fabs(R);
     }
   };
-  int kb = 0;
-  for (; kb + 64 * U <= n; kb += 64 * U) trip(kb, std::false_type{});
-  if (kb < n) trip(kb, std::true_type{});
-  const unsigned long long odd = __ballot(odd_int(sum));
-  if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
-  acc += sum;
-  accm += mag;
+  for (;;) {
+    int kb = 0;
+    for (; kb + 64 * U <= n; kb += 64 * U) trip(kb, std::false_type{});
+    if (kb < n) trip(kb, std::true_type{});
+    const unsigned long long odd = __ballot(odd_int(sum));
+    if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
+    acc += sum;
+    accm += mag;
+    if (++s >= s1) break;
+    // the next segment of the part starts where this one ended (a full one: SEGN sites, a
+    // multiple of the trip, so the look-ahead already holds its first trip)
+    seg_bounds<SEGN>(W, pt, s, ib, ie);
+    n = ie - ib;
+    sum = 0.0; mag = 0.0;
+  }
 }
 
 // a wave's share of walk w: int64 totals of sum R and sum |R| into S.P / S.Q.  Exact when
@@ -829,89 +843,99 @@ __device__ __forceinline__ unsigned long long ag_xchg64(unsigned long long* p, u
 }
 
 // Split cells: the members of a cell have each summed their segments of every walk into LDS;
-// add them up in the cell's XAcc region for this instance, meet at the cell's arrival counter,
-// and read the totals back, so that every member continues with identical values (resolve,
-// argmax and bisection then run redundantly and agree).  Every read of another member's data
-// is an atomic read-modify-write (add 0), served where the atomics were performed.  Member 0
-// zeroes the region of the previous instance (every member has read it before this
-// instance's arrival), in time for its reuse two instances later.  A member that waits
-// longer than ~1 s (the others never started: not co-resident) flags the cell and goes on.
+// each writes its sums, parity words and ties into its own slots of the cell's exchange area
+// for this instance, they meet at the cell's arrival counter (release / acquire at agent
+// scope: the members may sit on different XCDs), and every member reads all slots and
+// combines them identically, so that every member continues with the same values (resolve,
+// argmax and bisection then run redundantly and agree).  Three memory round trips: the
+// stores' completion, the arrival, the reads.  A member that waits longer than ~1 s (the
+// others never started: not co-resident) flags the cell and goes on.
 __device__ __forceinline__ void combine_members(Smem& S, const Params& P, int nw) {
   const int tid = threadIdx.x;
-  const int inst = S.inst;
-  XAcc* R = reinterpret_cast<XAcc*>(P.xacc + ((size_t)S.cell * 3 + (size_t)(inst % 3)) * sizeof(XAcc));
-  // 1. contribute
+  const int inst = S.inst, me = S.member, G = P.split;
+  XAcc* R = reinterpret_cast<XAcc*>(P.xacc + ((size_t)S.cell * 2 + (size_t)(inst & 1)) * sizeof(XAcc));
+  // 1. this member's slots
   if (tid < nw) {
-    if (S.P[tid]) ag_add64(&R->P[tid], S.P[tid]);
-    if (S.Q[tid]) ag_add64(&R->Q[tid], S.Q[tid]);
-    if (S.wflag[tid]) {
-      ag_or32(&R->wflag[tid], 1u);
-      ag_xchg64(reinterpret_cast<unsigned long long*>(&R->Pd[S.member][tid]),
-                (unsigned long long)__double_as_longlong(S.Pd[tid]));
-      ag_xchg64(reinterpret_cast<unsigned long long*>(&R->Qd[S.member][tid]),
-                (unsigned long long)__double_as_longlong(S.Qd[tid]));
-    }
-    for (int j = 0; j < SEGWORDS; j++)
-      if (S.segbits[tid][j]) ag_xor32(&R->segbits[tid][j], S.segbits[tid][j]);
+    R->P[me][tid] = S.P[tid];
+    R->Q[me][tid] = S.Q[tid];
+    R->wflag[me][tid] = (unsigned)S.wflag[tid];
+    R->Pd[me][tid] = S.Pd[tid];
+    R->Qd[me][tid] = S.Qd[tid];
+#pragma unroll
+    for (int j = 0; j < SEGWORDS; j++) R->segbits[me][tid][j] = S.segbits[tid][j];
   }
-  if (tid == 0) S.xbase = S.n_ties ? (int)ag_add32(&R->n_ties, (unsigned)S.n_ties) : 0;
-  __syncthreads();
   {
-    const int nt = min(S.n_ties, MAXTIES), base = S.xbase;
-    for (int t = tid; t < nt; t += WG)
-      if (base + t < MAXTIES) __hip_atomic_exchange(&R->ties[base + t], S.ties[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int nt = S.n_ties;
+    if (tid < min(nt, XTIES)) R->ties[me][tid] = S.ties[tid];
+    if (tid == 0) R->nt[me] = (unsigned)nt;
   }
   // 2. arrive (release) and wait for every member (acquire)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-#ifndef FSCLG_XP_NO_REL
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned int* cnt = P.xcnt + S.cell;
     ag_add32(cnt, 1u);
-    const unsigned int target = (unsigned)P.split * (unsigned)(inst + 1);
+    const unsigned int target = (unsigned)G * (unsigned)(inst + 1);
     const unsigned long long t0 = wall_clock64();
     while (ag_add32(cnt, 0u) < target) {
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > 100000000ull) { S.xfail = PF_SPLIT_TIMEOUT; break; }  // ~1 s at 100 MHz
     }
-#ifndef FSCLG_XP_NO_ACQ
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  // 3. the totals
+  // 3. every member's slots, combined (all loads of this step in flight together)
+  int tv = 0;
+  bool th = false;
+  {
+    const int m = tid / XTIES, k = tid % XTIES;
+    if (m < G) {
+      const unsigned int ntm = R->nt[m];
+      th = k < (int)min(ntm, (unsigned)XTIES);
+      if (th) tv = R->ties[m][k];
+    }
+  }
   if (tid < nw) {
-    S.P[tid] = ag_add64(&R->P[tid], 0ull);
-    S.Q[tid] = ag_add64(&R->Q[tid], 0ull);
-    S.wflag[tid] = (int)ag_or32(&R->wflag[tid], 0u);
-    if (S.wflag[tid]) {
+    unsigned long long pp = 0, qq = 0;
+    unsigned int fl = 0, sb[SEGWORDS];
+#pragma unroll
+    for (int j = 0; j < SEGWORDS; j++) sb[j] = 0;
+    for (int m = 0; m < G; m++) {
+      pp += R->P[m][tid];
+      qq += R->Q[m][tid];
+      fl |= R->wflag[m][tid];
+#pragma unroll
+      for (int j = 0; j < SEGWORDS; j++) sb[j] ^= R->segbits[m][tid][j];
+    }
+    S.P[tid] = pp; S.Q[tid] = qq; S.wflag[tid] = (int)fl;
+#pragma unroll
+    for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = sb[j];
+    if (fl) {
       double pd = 0.0, qd = 0.0;
-      for (int m = 0; m < P.split; m++) {  // member order: the same sum on every member
-        pd += __longlong_as_double((long long)ag_add64(reinterpret_cast<unsigned long long*>(&R->Pd[m][tid]), 0ull));
-        qd += __longlong_as_double((long long)ag_add64(reinterpret_cast<unsigned long long*>(&R->Qd[m][tid]), 0ull));
+      for (int m = 0; m < G; m++) {  // member order: the same sum on every member
+        if (R->wflag[m][tid]) { pd += R->Pd[m][tid]; qd += R->Qd[m][tid]; }
       }
       S.Pd[tid] = pd; S.Qd[tid] = qd;
     }
-    for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = ag_xor32(&R->segbits[tid][j], 0u);
   }
-  if (tid == 0) S.xbase = (int)ag_add32(&R->n_ties, 0u);
+  if (tid < G) S.xnt[tid] = (int)R->nt[tid];
   __syncthreads();
+  // 4. the ties, concatenated in member order (a member past XTIES: the overflow path)
   {
-    const int nt = min(S.xbase, MAXTIES);
-    for (int t = tid; t < nt; t += WG) S.ties[t] = (int)ag_add32(reinterpret_cast<unsigned int*>(&R->ties[t]), 0u);
-  }
-  __syncthreads();
-  if (tid == 0) S.n_ties = S.xbase;  // the total: above MAXTIES marks the overflow as before
-  // 4. member 0 clears the previous instance's region (read by every member before this arrival)
-  if (S.member == 0) {
-    XAcc* Z = reinterpret_cast<XAcc*>(P.xacc + ((size_t)S.cell * 3 + (size_t)((inst + 2) % 3)) * sizeof(XAcc));
-    unsigned int* z = reinterpret_cast<unsigned int*>(Z);
-    for (int k = tid; k < (int)(sizeof(XAcc) / 4); k += WG)
-      __hip_atomic_exchange(z + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int m = tid / XTIES, k = tid % XTIES;
+    int base = 0, tot = 0;
+    bool over = false;
+    for (int j = 0; j < G; j++) {
+      const int n = S.xnt[j];
+      if (j < m) base += min(n, XTIES);
+      tot += n;
+      over = over || n > XTIES;
+    }
+    if (th) S.ties[base + k] = tv;
+    if (tid == 0) S.n_ties = over ? MAXTIES + 1 : tot;  // above MAXTIES marks the overflow as before
   }
   if (tid == 0) S.inst = inst + 1;
   __syncthreads();
@@ -1003,7 +1027,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   // miscompiled into a loop that never re-issued its atomic)
   {
     const int ngrp = __builtin_amdgcn_readfirstlane(S.ngrp);
-    int k = 0, cw = -1, nsg = 0;
+    int k = 0, cw = -1, nsg_run = 0;
     double acc = 0.0, accm = 0.0;
     for (int gi = 0; gi < ngrp; gi++) {
      const int gwb = __builtin_amdgcn_readfirstlane(S.gwb[gi]);
@@ -1023,12 +1047,13 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
         if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
         cw = w; acc = 0.0; accm = 0.0;
       }
-      run_segment_idx<LDS, SEGN, SPLIT ? U_SPLIT : U_MAIN>(S, w, g - S.w[w].seg0, P, lane, acc, accm);
-      nsg++;
+      run_segment_idx<LDS, SEGN, SPLIT ? U_SPLIT : U_MAIN>(S, w, g - S.w[w].seg0, g - S.w[w].seg0 + 1, P, lane, acc,
+                                                           accm);
+      nsg_run++;
      }
     }
     if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
-    IEV(3, nsg, 0);  // wave 0's segments done
+    IEV(3, nsg_run, 0);  // wave 0's segment runs done
   }
   PHASE_MARK(1);
   __syncthreads();
@@ -2316,7 +2341,7 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
     c->n_ep_saved += (unsigned long long)(2 * nu - ne);
   }
   if (G > 1) {
-    const size_t xb = (size_t)nl * 3 * sizeof(XAcc);
+    const size_t xb = (size_t)nl * 2 * sizeof(XAcc);
     if (B.xacc_cap < xb) {
       if (B.d_xacc) hipFree(B.d_xacc);
       B.d_xacc = nullptr; B.xacc_cap = 0;
@@ -2324,8 +2349,8 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
       B.xacc_cap = xb;
     }
     if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, nl))) return r;
-    HIPCHK(hipMemsetAsync(B.d_xacc, 0, xb, B.stream), "hipMemsetAsync");
-    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");
+    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");  // the exchange
+                                                                                                  // areas need no zeroing
     P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
     // latency: no LDS coefficient windows (their loads, repeated by every member for every
     // phase, cost more than the global gathers of a lightly loaded device)
