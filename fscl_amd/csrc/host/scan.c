@@ -1609,6 +1609,15 @@ void fscl_amd_get_stats(fscl_amd_stats_t *st) {
       st->cache_cover = g.cache_cover;
     }
   }
+  if (DI.ctx) {  /* the drop-in search_maxalpha's own context */
+    fsclg_stats_t g;
+    if (fsclg_get_stats(DI.ctx, &g) == FSCLG_OK) {
+      st->kernel_ms += g.kernel_ms;
+      st->n_terms += g.n_terms; st->n_walks += g.n_walks; st->n_maxalpha += g.n_maxalpha;
+      st->n_launches += g.n_launches;
+      st->busy_ms += g.busy_ms;
+    }
+  }
   st->n_devices = D.n_dev;
 }
 
@@ -1616,6 +1625,7 @@ void fscl_amd_reset_stats(void) {
   int l;
   memset(&D.st, 0, sizeof D.st);
   for (l = 0; l < D.n_dev; l++) fsclg_reset_stats(D.ctx[l]);
+  if (DI.ctx) fsclg_reset_stats(DI.ctx);
 }
 
 void fscl_amd_shutdown(void) {
