@@ -489,13 +489,11 @@ __device__ __forceinline__ void walk_bounds_par(Smem& S, const Params& P, int ti
 // the chunk is added term by term as the reference does.  Walks that leave the binade of the
 // window null sum (ascertainment-corrected tables: sums far below null) cross a few binades,
 // so almost every chunk takes the reduction.
-template <bool LDS>
-__device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, const Params& P, int lane) {
-  double acc = pt.N;
-  for (int kb = 0; kb < W.len; kb += 64) {
-    const int k = kb + lane;
-    double t = 0.0;
-    if (k < W.len) t = term_dev<LDS>(walk_index(k, pt.nearest, W.nl), pt.sweep, W.la, S, P);
+// acc + t_0 + t_1 + ... + t_{lim-1} in that order, exactly as the sequential fp adds do, for
+// one wave whose lane l holds t_l (lanes >= lim hold 0.0): one wave reduction when the chunk
+// provably stays in acc's binade with no tie, else term by term
+__device__ __forceinline__ double exact_chunk_add(double acc, double t, int lim) {
+  {
     const unsigned long long bits = (unsigned long long)__double_as_longlong(acc);
     const int be = (int)((bits >> 52) & 0x7FF);
     if (acc < 0.0 && be > 52 && be < 0x7FF - 52) {
@@ -509,14 +507,23 @@ __device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, 
         const double A0 = acc * inv;  // an integer in (-2^53, -2^52]
         // every partial lies in [A0 + sn, A0 + sp]; inside (-2^53, -2^52] it stays in the binade
         if (sp < 9007199254740992.0 && sn > -9007199254740992.0 && A0 + sn > -9007199254740992.0 &&
-            A0 + sp <= -4503599627370496.0) {
-          acc = (A0 + sp + sn) * u;
-          continue;
-        }
+            A0 + sp <= -4503599627370496.0)
+          return (A0 + sp + sn) * u;
       }
     }
-    const int lim = W.len - kb < 64 ? W.len - kb : 64;
-    for (int l = 0; l < lim; l++) acc = acc + __shfl(t, l, 64);
+  }
+  for (int l = 0; l < lim; l++) acc = acc + __shfl(t, l, 64);
+  return acc;
+}
+
+template <bool LDS>
+__device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, const Params& P, int lane) {
+  double acc = pt.N;
+  for (int kb = 0; kb < W.len; kb += 64) {
+    const int k = kb + lane;
+    double t = 0.0;
+    if (k < W.len) t = term_dev<LDS>(walk_index(k, pt.nearest, W.nl), pt.sweep, W.la, S, P);
+    acc = exact_chunk_add(acc, t, W.len - kb < 64 ? W.len - kb : 64);
     if (acc != acc) break;  // NaN stays NaN through every later add (NaN spline rows, Q15)
   }
   return acc;
@@ -1352,10 +1359,13 @@ search_maxpos_split_kernel(Params P) {
 // block stages the elements its 1024 windows span through an LDS tile.
 constexpr int WN_WG = 256, WN_PER = 4, WN_TILE = 4096;
 
-__global__ void __launch_bounds__(WN_WG) window_null_kernel(const uint2* __restrict__ pr,
-                                                            const double* __restrict__ nullrow,
-                                                            const int2* __restrict__ tasks, int W,
-                                                            double* __restrict__ out) {
+// A block's staging of a tile is one round of independent row loads (all of a full tile's rows
+// before any null value), and its sums read the tile eight elements at a time before adding
+// them: each window's chain of adds then runs at the FP64 add latency, not one LDS round trip
+// per element (measured: 20 ms per C5 x 4 launch before, one read and four adds per element).
+__global__ void __launch_bounds__(WN_WG)
+window_null_kernel(const uint2* __restrict__ pr, const double* __restrict__ nullrow, const int2* __restrict__ tasks,
+                   int W, double* __restrict__ out) {
   __shared__ double tile[WN_TILE];
   const int2 t = tasks[blockIdx.x];  // windows [t.x, t.x + t.y)
   const int k = threadIdx.x;
@@ -1366,7 +1376,15 @@ __global__ void __launch_bounds__(WN_WG) window_null_kernel(const uint2* __restr
   for (int T0 = t.x; T0 < end; T0 += WN_TILE) {
     const int T1 = min(T0 + WN_TILE, end);
     __syncthreads();
-    for (int j = T0 + k; j < T1; j += WN_WG) tile[j - T0] = nullrow[pr[j].y];
+    if (T1 - T0 == WN_TILE) {
+      uint32_t rr[WN_TILE / WN_WG];
+#pragma unroll
+      for (int q = 0; q < WN_TILE / WN_WG; q++) rr[q] = pr[T0 + k + q * WN_WG].y;
+#pragma unroll
+      for (int q = 0; q < WN_TILE / WN_WG; q++) tile[k + q * WN_WG] = nullrow[rr[q]];
+    } else {
+      for (int j = T0 + k; j < T1; j += WN_WG) tile[j - T0] = nullrow[pr[j].y];
+    }
     __syncthreads();
     if (nwin == 0) continue;
     const int lo = max(T0, base), hi = min(T1, base + nwin - 1 + W);
@@ -1384,7 +1402,15 @@ __global__ void __launch_bounds__(WN_WG) window_null_kernel(const uint2* __restr
     if (nwin < WN_PER) { edge(lo, hi); continue; }
     const int m0 = min(max(lo, base + WN_PER - 1), hi), m1 = max(min(hi, base + W), m0);
     edge(lo, m0);
-    for (int j = m0; j < m1; j++) {  // every window of the thread takes these
+    int j = m0;
+    for (; j + 8 <= m1; j += 8) {  // every window of the thread takes these, each in order
+      double v[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) v[q] = tile[j - T0 + q];
+#pragma unroll
+      for (int q = 0; q < 8; q++) { a0 += v[q]; a1 += v[q]; a2 += v[q]; a3 += v[q]; }
+    }
+    for (; j < m1; j++) {
       const double v = tile[j - T0];
       a0 += v; a1 += v; a2 += v; a3 += v;
     }

@@ -1,0 +1,6 @@
+# BASELINE configs[4] at full size: C5 (5.0M SNPs, n=400, 50k cells, 10 000 permutations, early prune), one GPU
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/r02z
+mkdir -p $OUT
+FSCL_AMD_TRIAL_TRACE=$OUT/tt_c5.txt timeout -k 10 1100 python -u bench.py --config C5 --warmup 0 --steps 1 --no-cpu-baseline > $OUT/c5_full.json 2> $OUT/c5_full.err
