@@ -105,6 +105,7 @@ EXPORTS = [
     "fsclg_upload_snps", "fsclg_set_rows", "fsclg_set_chr_null", "fsclg_set_alpha_grid", "fsclg_search_maxpos",
     "fsclg_search_points", "fsclg_get_stats", "fsclg_reset_stats", "fsclg_interval_thresholds",
     "fsclg_row_buffer", "fsclg_slot_row_buffer", "fsclg_slot_set_rows", "fsclg_search_submit", "fsclg_search_wait",
+    "fsclg_slot_windows",
 ]
 
 

@@ -1363,16 +1363,22 @@ constexpr int WN_WG = 256, WN_PER = 4, WN_TILE = 4096;
 // before any null value), and its sums read the tile eight elements at a time before adding
 // them: each window's chain of adds then runs at the FP64 add latency, not one LDS round trip
 // per element (measured: 20 ms per C5 x 4 launch before, one read and four adds per element).
+template <int WPER>
 __global__ void __launch_bounds__(WN_WG)
 window_null_kernel(const uint2* __restrict__ pr, const double* __restrict__ nullrow, const int2* __restrict__ tasks,
                    int W, double* __restrict__ out) {
   __shared__ double tile[WN_TILE];
+  // the search kernels' waves share these SIMDs and wait on memory most of their cycles; a
+  // trial's cells wait for these sums, so their waves issue first
+  __builtin_amdgcn_s_setprio(2);
   const int2 t = tasks[blockIdx.x];  // windows [t.x, t.x + t.y)
   const int k = threadIdx.x;
-  const int base = t.x + WN_PER * k;
-  const int nwin = min(max(t.y - WN_PER * k, 0), WN_PER);
+  const int base = t.x + WPER * k;
+  const int nwin = min(max(t.y - WPER * k, 0), WPER);
   const int end = t.x + t.y - 1 + W;  // one past the last element a window of the block uses
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  double a[WPER];
+#pragma unroll
+  for (int m = 0; m < WPER; m++) a[m] = 0.0;
   for (int T0 = t.x; T0 < end; T0 += WN_TILE) {
     const int T1 = min(T0 + WN_TILE, end);
     __syncthreads();
@@ -1393,14 +1399,13 @@ window_null_kernel(const uint2* __restrict__ pr, const double* __restrict__ null
       for (int j = j0; j < j1; j++) {
         const double v = tile[j - T0];
         const int off = j - base;
-        if (off < W) a0 += v;
-        if (nwin > 1 && off >= 1 && off < W + 1) a1 += v;
-        if (nwin > 2 && off >= 2 && off < W + 2) a2 += v;
-        if (nwin > 3 && off >= 3 && off < W + 3) a3 += v;
+#pragma unroll
+        for (int m = 0; m < WPER; m++)
+          if (m < nwin && off >= m && off < W + m) a[m] += v;
       }
     };
-    if (nwin < WN_PER) { edge(lo, hi); continue; }
-    const int m0 = min(max(lo, base + WN_PER - 1), hi), m1 = max(min(hi, base + W), m0);
+    if (nwin < WPER) { edge(lo, hi); continue; }
+    const int m0 = min(max(lo, base + WPER - 1), hi), m1 = max(min(hi, base + W), m0);
     edge(lo, m0);
     int j = m0;
     for (; j + 8 <= m1; j += 8) {  // every window of the thread takes these, each in order
@@ -1408,18 +1413,20 @@ window_null_kernel(const uint2* __restrict__ pr, const double* __restrict__ null
 #pragma unroll
       for (int q = 0; q < 8; q++) v[q] = tile[j - T0 + q];
 #pragma unroll
-      for (int q = 0; q < 8; q++) { a0 += v[q]; a1 += v[q]; a2 += v[q]; a3 += v[q]; }
+      for (int q = 0; q < 8; q++)
+#pragma unroll
+        for (int m = 0; m < WPER; m++) a[m] += v[q];
     }
     for (; j < m1; j++) {
       const double v = tile[j - T0];
-      a0 += v; a1 += v; a2 += v; a3 += v;
+#pragma unroll
+      for (int m = 0; m < WPER; m++) a[m] += v;
     }
     edge(m1, hi);
   }
-  if (nwin > 0) out[base] = a0;
-  if (nwin > 1) out[base + 1] = a1;
-  if (nwin > 2) out[base + 2] = a2;
-  if (nwin > 3) out[base + 3] = a3;
+#pragma unroll
+  for (int m = 0; m < WPER; m++)
+    if (m < nwin) out[base + m] = a[m];
 }
 
 // one trial's rows into the (position, row) array: pr[i].y = row[i] + 1 (device row), read
@@ -1460,7 +1467,11 @@ struct Slot {
   double* d_chr_null = nullptr;
   double* d_win_null = nullptr;   // [n_snps], valid for (win_er, rows) while win_valid
   int win_er = -1;
-  bool win_valid = false;
+  bool win_valid = false;         // win_null holds every window start, or (win_part) the ranges wdone
+  bool win_part = false;
+  std::vector<int2> wdone;        // window starts [x, y) summed for the slot's rows, sorted, disjoint
+  int2* p_wtasks = nullptr;       // pinned: the tasks of the slot's last partial window launch
+  int wtask_cap = 0;
   uint32_t* h_rows = nullptr;     // pinned (coherent) staging of one trial's rows, read by scatter_rows_kernel
   double* h_null = nullptr;       // pinned (coherent) whole-chromosome null sums, n_chr
   int rows_cap = 0, null_cap = 0;
@@ -1668,7 +1679,7 @@ int fsclg_close(fsclg_ctx* c) {
   for (void* p : ptrs) if (p) hipFree(p);
   for (Slot& S : c->slot) {
     for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null}) if (p) hipFree(p);
-    for (void* p : {(void*)S.h_rows, (void*)S.h_null}) if (p) hipHostFree(p);
+    for (void* p : {(void*)S.h_rows, (void*)S.h_null, (void*)S.p_wtasks}) if (p) hipHostFree(p);
     hipEventDestroy(S.ready);
     if (S.wev0) hipEventDestroy(S.wev0);
     if (S.wev1) hipEventDestroy(S.wev1);
@@ -1991,9 +2002,28 @@ static int window_time(fsclg_ctx* c, Slot& S) {
 // the null sums of every window of the chromosomes longer than 2*er+1 SNPs, for the slot's
 // rows (window_null_kernel on the upload stream, timed apart from the search; the host does
 // not wait for it: the slot's batches wait on the GPU, and its time is read later)
-static int ensure_windows(fsclg_ctx* c, int slot, int er) {
+static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out);
+static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vector<int2>& todo);
+
+static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* cells, int n_cells) {
   const long long W = 2ll * er + 1;
   Slot& S = c->slot[slot];
+  if (S.win_valid && S.win_er == er && S.win_part) {  // fsclg_slot_windows summed some: anything missing?
+    std::vector<int2> need, todo;
+    window_ranges(c, er, cells, n_cells, need);
+    size_t d = 0;
+    for (int2 x : need) {
+      int a = x.x;
+      while (d < S.wdone.size() && S.wdone[d].y <= a) d++;
+      for (size_t e = d; e < S.wdone.size() && S.wdone[e].x < x.y && a < x.y; e++) {
+        if (S.wdone[e].x > a) todo.push_back(make_int2(a, S.wdone[e].x));
+        a = std::max(a, S.wdone[e].y);
+      }
+      if (a < x.y) todo.push_back(make_int2(a, x.y));
+    }
+    if (todo.empty()) return FSCLG_OK;
+    return launch_partial_windows(c, S, er, todo);
+  }
   if (S.win_valid && S.win_er == er) return FSCLG_OK;
   if (c->wtask_er != er) {
     std::vector<int2> tasks;
@@ -2024,7 +2054,7 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er) {
     int r;
     if ((r = window_time(c, S))) return r;  // the slot's previous launch (long finished)
     HIPCHK(hipEventRecord(S.wev0, c->ustream), "hipEventRecord");
-    hipLaunchKernelGGL(window_null_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
+    hipLaunchKernelGGL((window_null_kernel<WN_PER>), dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
                        c->d_wtasks, (int)W, S.d_win_null);
     HIPCHK(hipGetLastError(), "launch window_null_kernel");
     HIPCHK(hipEventRecord(S.wev1, c->ustream), "hipEventRecord");
@@ -2033,7 +2063,111 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er) {
   }
   S.win_er = er;
   S.win_valid = true;
+  S.win_part = false;
+  S.wdone.clear();
   return FSCLG_OK;
+}
+
+// the window starts a set of cells can read (one range per cell: a bisection point of the cell
+// [start, end] has its nearest SNP in [j(start) - 1, j(end)], search_snppos's j being the least
+// index in [1, n) with position >= pos (n if none), and the window start is monotone in the
+// nearest SNP), merged, for the chromosomes above 2*er+1 SNPs
+static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out) {
+  const long long W = 2ll * er + 1;
+  std::vector<int2> need;
+  for (int i = 0; i < n_cells; i++) {
+    const int ch = cells[i].chr;
+    if (ch < 0 || ch >= c->n_chr) continue;
+    const long long n = c->h_chr_n[ch];
+    if (n <= W) continue;
+    const int cs = c->h_chr_start[ch], ce = cs + (int)n - 1;
+    const int32_t* pos = c->h_pos.data() + cs;
+    auto jof = [&](int x) { return (int)(std::lower_bound(pos + 1, pos + n, x) - pos); };
+    const int nlo = std::max(jof(cells[i].start_pos) - 1, 0), nhi = std::min(jof(cells[i].end_pos), (int)n - 1);
+    auto wsof = [&](int nl) {
+      const int near = cs + nl;
+      if (near - er < cs) return cs;
+      if (near + er > ce) return std::max(cs, (int)(ce - 2ll * er));
+      return near - er;
+    };
+    need.push_back(make_int2(wsof(nlo), wsof(nhi) + 1));
+  }
+  std::sort(need.begin(), need.end(), [](int2 a, int2 b) { return a.x < b.x; });
+  out.clear();
+  for (const int2& x : need) {
+    if (!out.empty() && x.x <= out.back().y) out.back().y = std::max(out.back().y, x.y);
+    else out.push_back(x);
+  }
+  return FSCLG_OK;
+}
+
+// sum the window starts todo (disjoint, sorted) for the slot's rows and add them to wdone
+static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vector<int2>& todo) {
+  // one window per thread (the latency of one sequential chain per window, not four)
+  long long blocks = 0;
+  for (const int2& x : todo) blocks += (x.y - x.x + WN_WG - 1) / WN_WG;
+  if (!blocks) return FSCLG_OK;
+  // the slot's previous window launch has read its task list (launches on one stream, in order)
+  if (S.wpend) HIPCHK(hipEventSynchronize(S.wev1), "hipEventSynchronize");
+  if (S.wtask_cap < blocks) {
+    if (S.p_wtasks) hipHostFree(S.p_wtasks);
+    S.p_wtasks = nullptr; S.wtask_cap = 0;
+    HIPCHK(hipHostMalloc((void**)&S.p_wtasks, sizeof(int2) * blocks, HOSTMEM), "hipHostMalloc window tasks");
+    S.wtask_cap = (int)blocks;
+  }
+  int nt = 0;
+  for (const int2& x : todo)
+    for (int o = x.x; o < x.y; o += WN_WG) S.p_wtasks[nt++] = make_int2(o, std::min(WN_WG, x.y - o));
+  int r;
+  if ((r = window_time(c, S))) return r;
+  HIPCHK(hipEventRecord(S.wev0, c->ustream), "hipEventRecord");
+  hipLaunchKernelGGL((window_null_kernel<1>), dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
+                     (int)(2ll * er + 1), S.d_win_null);
+  HIPCHK(hipGetLastError(), "launch window_null_kernel");
+  HIPCHK(hipEventRecord(S.wev1, c->ustream), "hipEventRecord");
+  HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");  // the slot's batches wait for it on the GPU
+  S.wpend = true;
+  std::vector<int2> u(S.wdone);
+  u.insert(u.end(), todo.begin(), todo.end());
+  std::sort(u.begin(), u.end(), [](int2 a, int2 b) { return a.x < b.x; });
+  S.wdone.clear();
+  for (const int2& x : u) {
+    if (!S.wdone.empty() && x.x <= S.wdone.back().y) S.wdone.back().y = std::max(S.wdone.back().y, x.y);
+    else S.wdone.push_back(x);
+  }
+  S.win_er = er; S.win_valid = true; S.win_part = true;
+  return FSCLG_OK;
+}
+
+// A trial's window null sums for the cells every batch on the slot will evaluate (all of them,
+// before the slot's first submit): only those windows when they are few (the pruned tail of a
+// long permutation test: a few hundred cells), every window otherwise.  One launch per trial.
+int fsclg_slot_windows(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, int n_cells, int eval_range) {
+  if (!c || slot < 0 || slot >= NSLOT || (!cells && n_cells) || n_cells < 0 || eval_range < 0)
+    return set_err(FSCLG_E_ARG, "slot windows");
+  if (!c->d_pr0) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  Slot& S = c->slot[slot];
+  if (S.users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  const long long W = 2ll * eval_range + 1;
+  // cost in waves with windows to sum (a wave: 64 threads x WN_PER windows; a block's waves
+  // without windows only stage tiles)
+  constexpr int WW = 64 * WN_PER;
+  long long all = 0;
+  for (int ch = 0; ch < c->n_chr; ch++)
+    if (c->h_chr_n[ch] > W) all += (c->h_chr_n[ch] - W + 1 + WW - 1) / WW;
+  if (!all) return FSCLG_OK;  // no chromosome above the window: the whole-chromosome sums serve
+  std::vector<int2> need;
+  window_ranges(c, eval_range, cells, n_cells, need);
+  long long waves = 0;
+  for (const int2& x : need) waves += (x.y - x.x + WW - 1) / WW;
+  if (2 * waves >= all) {  // most windows: every one, the dense kernel's way
+    S.win_valid = false;
+    return ensure_windows(c, slot, eval_range, nullptr, 0);
+  }
+  S.wdone.clear();
+  S.win_valid = false;
+  return launch_partial_windows(c, S, eval_range, need);
 }
 
 
@@ -2208,7 +2342,7 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
     c->slot[slot].users++;
     return FSCLG_OK;
   }
-  if ((r = ensure_windows(c, slot, eval_range))) return r;
+  if ((r = ensure_windows(c, slot, eval_range, cells, n_cells))) return r;
   // identical cells are evaluated once (permutation cells are G-aligned, so two points can
   // share one), and so is an endpoint shared by neighbouring cells (scan-chromosome.c:130-134
   // evaluates both ends of every cell): a first launch evaluates the distinct endpoints, the

@@ -1029,9 +1029,10 @@ static void tb_reserve(trial_batch_t *b, int n) {
 
 static void tb_free(trial_batch_t *b) { free(b->pt); free(b->cells); free(b->out); memset(b, 0, sizeof *b); }
 
-static void tb_submit(trial_batch_t *b, int slot, int eval_range, int bp_resl) {
+/* the local devices' shares of a batch, fixed at planning */
+static void tb_plan(trial_batch_t *b, int eval_range) {
   double *cost = NULL;
-  int i, l;
+  int i;
   if (D.world * D.n_dev > 1) {
     /* a point's measured cell cost from its last trial, else its window size (~32 terms /
        1024 per window site) */
@@ -1041,6 +1042,25 @@ static void tb_submit(trial_batch_t *b, int slot, int eval_range, int bp_resl) {
   }
   dev_shares(cost, b->n, b->lo, b->hi);
   free(cost);
+}
+
+/* each local device's window null sums for its shares of a trial's two batches, before their
+   submits (the pruned tail: only the few active cells' windows) */
+static void trial_windows(int slot, const trial_batch_t *a, const trial_batch_t *b, int eval_range) {
+  fsclg_cell_t *tmp = NULL;
+  int l;
+  for (l = 0; l < D.n_dev; l++) {
+    const int na = a->hi[l] - a->lo[l], nb = b->hi[l] - b->lo[l];
+    tmp = fh_realloc(tmp, sizeof(fsclg_cell_t) * (na + nb ? na + nb : 1), "cells");
+    memcpy(tmp, a->cells + a->lo[l], sizeof(fsclg_cell_t) * (size_t)na);
+    memcpy(tmp + na, b->cells + b->lo[l], sizeof(fsclg_cell_t) * (size_t)nb);
+    dev_check(fsclg_slot_windows(D.ctx[l], slot, tmp, na + nb, eval_range), "window sums");
+  }
+  free(tmp);
+}
+
+static void tb_submit(trial_batch_t *b, int slot, int eval_range, int bp_resl) {
+  int l;
   for (l = 0; l < D.n_dev; l++) {
     dev_check(fsclg_search_submit(D.ctx[l], b->batch, slot, b->cells + b->lo[l], b->hi[l] - b->lo[l], eval_range,
                                   bp_resl),
@@ -1222,6 +1242,9 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     /* both batches always go through submit / wait (an empty share is a no-op), so that
        every rank takes part in the same exchanges */
     tr[3] = fh_now();
+    tb_plan(&A, eval_range);
+    tb_plan(B, eval_range);
+    trial_windows(slot, &A, B, eval_range);
     tb_submit(&A, slot, eval_range, bp_resl);
     tb_submit(B, slot, eval_range, bp_resl);
     /* while the GPUs work: the next trial's permutation for this trial's likely draw counts */

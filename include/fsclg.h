@@ -119,6 +119,11 @@ int fsclg_set_rows(fsclg_ctx *c, const uint32_t *row);
    synchronous calls (fsclg_set_rows, fsclg_search_maxpos) use. */
 uint32_t *fsclg_slot_row_buffer(fsclg_ctx *c, int slot);
 int fsclg_slot_set_rows(fsclg_ctx *c, int slot, const uint32_t *row, const double *chr_null);
+/* the window null sums (chromosomes above 2*eval_range+1 SNPs) for the cells that the slot's
+   next batches will evaluate, given before the slot's first submit of a trial: only those
+   windows when they are few, every window otherwise (a batch whose cells need windows not
+   summed yet sums them at its submit) */
+int fsclg_slot_windows(fsclg_ctx *c, int slot, const fsclg_cell_t *cells, int n_cells, int eval_range);
 int fsclg_search_submit(fsclg_ctx *c, int batch, int slot, const fsclg_cell_t *cells, int n_cells, int eval_range,
                         int bp_resl);
 int fsclg_search_wait(fsclg_ctx *c, int batch, fsclg_point_t *out);
