@@ -105,7 +105,7 @@ EXPORTS = [
     "fsclg_upload_snps", "fsclg_set_rows", "fsclg_set_chr_null", "fsclg_set_alpha_grid", "fsclg_search_maxpos",
     "fsclg_search_points", "fsclg_get_stats", "fsclg_reset_stats", "fsclg_interval_thresholds",
     "fsclg_row_buffer", "fsclg_slot_row_buffer", "fsclg_slot_set_rows", "fsclg_search_submit", "fsclg_search_wait",
-    "fsclg_slot_windows",
+    "fsclg_slot_windows", "ms_openfile", "ms_background", "ms_next_block",
 ]
 
 
@@ -117,6 +117,9 @@ def _load() -> C.CDLL:
     sigs = {
         "load_snp_input": (P(ScanT), [C.c_char_p, C.c_int, C.c_int]),
         "fscl_amd_load_ms_input": (P(ScanT), [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "ms_openfile": (None, [C.c_char_p]),
+        "ms_background": (P(ScanT), [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "ms_next_block": (P(ScanT), [C.c_int, C.c_int, C.c_int, C.c_int]),
         "background_fsp": (P(P(C.c_double)), [P(ScanT), C.c_int, C.c_char_p, C.c_int]),
         "output_background_fs": (None, [C.c_char_p, P(ScanT), P(P(C.c_double))]),
         "lchoose": (C.c_double, [C.c_int, C.c_int]),
@@ -194,6 +197,18 @@ def load_snp_input(path, include_invariant: bool = False, minimum_depth: int = 5
 def load_ms_input(path, segment_length: int, folded: bool = False, sample_first: int = 0, sample_size: int = 0):
     return get_lib().fscl_amd_load_ms_input(_b(path), int(segment_length), int(folded), int(sample_first),
                                       int(sample_size))
+
+
+def ms_blocks(path, segment_length: int, folded: bool = False, sample_first: int = 0, sample_size: int = 0):
+    """The reference's block loop (fscl.c:296-313): ms_openfile, then one
+    scan_t per ms_next_block until it returns NULL."""
+    L = get_lib()
+    L.ms_openfile(_b(path))
+    while True:
+        s = L.ms_next_block(int(segment_length), int(folded), int(sample_first), int(sample_size))
+        if not s:
+            return
+        yield s
 
 
 def background_fsp(scan, force_neutral: bool = False, bs_file=None, include_invariant: bool = False):

@@ -22,6 +22,7 @@
  *   scan_chromosome            fscl.h:109  scan-chromosome.c:228-329 (GPU)
  *   scan_permute               fscl.h:111  scan-chromosome.c:582-652 (GPU + host permutation)
  *   scan_output                fscl.h:115  scan-chromosome.c:666-750
+ *   ms_openfile/ms_background/ms_next_block fscl.h:118-123 ms-input.c:11-151
  *   ascbias_adjust_background  fscl.h:126  asc-bias.c:27-95
  *   ascbias_adjust_expect      fscl.h:128  asc-bias.c:97-109
  *   configure_logmsg/logmsg/cr_logmsg fscl.h:134-136 logmsg.c:20-52
@@ -127,6 +128,13 @@ void scan_chromosome(scan_t *scan_obj, sm_ptable_t *sm_p, int eval_range, int bp
 void scan_permute(scan_t *scan_obj, sm_ptable_t *sm_p, int n_permute, double permute_nbp, double alpha_factor,
                   int n_threads, int eval_range, int bp_resl, int large_grid_sp, double scan_width_mb);
 void scan_output(char *output_fname, scan_t *scan_obj, int maximum_only, int n_permute, char *prepend_label);
+/* ms input block by block (fscl.h:118-123, ms-input.c; called at fscl.c:281-313),
+   with fscl_amd_load_ms_input's semantics: ms_background = every block,
+   ms_next_block = the next block as a one-chromosome scan_t, NULL at the end */
+void ms_openfile(char *ms_fname);
+scan_t *ms_background(char *ms_fname, int ms_segment_length, int ms_folded, int ms_sample_first,
+                      int ms_sample_size);
+scan_t *ms_next_block(int ms_segment_length, int ms_folded, int ms_sample_first, int ms_sample_size);
 double *ascbias_adjust_background(double *bsf, int n, int asc_depth, int min_obs);
 void ascbias_adjust_expect(double *fsp, int n, int min_obs, int d);
 void configure_logmsg(int level);

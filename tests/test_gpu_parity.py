@@ -166,6 +166,31 @@ def test_ms_input_matches_oracle_on_converted_file(built, tmp):
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
 
 
+def test_ms_block_loop_matches_whole_file(built, tmp):
+    """fscl.c's ms loop (fscl.c:281-313) through the C-ABI: tables from ms_background's
+    spectrum, then compute_snp_null_model / scan_chromosome / scan_output per ms_next_block
+    scan_t.  The blocks' outputs, concatenated, are the whole-file scan's output, which
+    test_ms_input_matches_oracle_on_converted_file pins to the oracle."""
+    ms = tmp / "x.ms"
+    synth.write_ms_file(str(ms), n_blocks=3, n_hap=20, n_seg=500, seed=43)
+    r = subprocess.run([str(CLI), "-m", str(ms), "--ms-segment-length=2000000", "-o", str(tmp / "g.txt"),
+                        "-G", "50000"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    L = fscl_amd.get_lib()
+    bg = L.ms_background(str(ms).encode(), 2_000_000, 0, 0, 0)
+    fsp = fscl_amd.background_fsp(bg)
+    tab = fscl_amd.compute_sweep_model_tables(bg, fsp)
+    out = []
+    for b, s in enumerate(fscl_amd.ms_blocks(ms, 2_000_000)):
+        assert s.contents.n_snps > 0
+        fscl_amd.compute_snp_null_model(s, fsp)
+        fscl_amd.scan_chromosome(s, tab, large_grid_sp=50000)
+        L.scan_output(str(tmp / f"b{b}.txt").encode(), s, 0, 0, None)
+        out.append((tmp / f"b{b}.txt").read_text())
+    assert len(out) == 3
+    assert "".join(out) == (tmp / "g.txt").read_text()
+
+
 def test_search_maxalpha_dropin(built):
     """search_maxalpha() on caller-initialised points (the reference's own scan loop calls it per
     point, scan-chromosome.c:126-135) equals the golden points, every one of them.  Its tables

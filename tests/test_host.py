@@ -170,6 +170,37 @@ def test_ms_reader_semantics(built, tmp):
                for k in range(s_f.n_snps))
 
 
+def test_ms_block_interface(built, tmp):
+    """ms_background / ms_openfile / ms_next_block (fscl.h:118-123) as fscl.c:281-313 drives
+    them: the background is every block, then one single-chromosome scan_t per block (a block
+    without polymorphic sites gives n_snps 0), then NULL."""
+    ms = tmp / "x.ms"
+    synth.write_ms_file(str(ms), n_blocks=3, n_hap=12, n_seg=40, seed=5)
+    with open(ms, "a") as f:  # a fourth block whose sites are all monomorphic in the sample
+        f.write("\n//\nsegsites: 2\npositions: 0.25 0.5\n" + "11\n" * 12)
+    L = fscl_amd.get_lib()
+    whole = fscl_amd.load_ms_input(ms, 1_000_000).contents
+    bg = L.ms_background(str(ms).encode(), 1_000_000, 0, 0, 0).contents
+    snps = lambda s: [(s.snps[k].chr, s.snps[k].pos, s.snps[k].obs_freq, s.snps[k].folded,
+                       s.sample_depths[s.snps[k].depth_p]) for k in range(s.n_snps)]
+    assert snps(bg) == snps(whole) and bg.n_chromosomes == whole.n_chromosomes
+    blocks = list(fscl_amd.ms_blocks(ms, 1_000_000))
+    assert len(blocks) == 4
+    for b, sp in enumerate(blocks):
+        s = sp.contents
+        assert s.n_chromosomes == 1 and s.chr_limits[0].name.decode() == str(b + 1)
+        want = [(0, *w[1:]) for w in snps(whole) if w[0] == b]
+        assert snps(s) == want
+        if want:
+            cl = s.chr_limits[0]
+            assert (cl.start_index, cl.n_snps, cl.start_pos) == (0, len(want), want[0][1])
+    assert blocks[3].contents.n_snps == 0
+    # reopening restarts at the first block; folded and a sub-sample are passed through
+    f1 = next(fscl_amd.ms_blocks(ms, 1_000_000, folded=True, sample_first=2, sample_size=8)).contents
+    w1 = fscl_amd.load_ms_input(ms, 1_000_000, folded=True, sample_first=2, sample_size=8).contents
+    assert snps(f1) == [w for w in snps(w1) if w[0] == 0]
+
+
 def test_partition_is_contiguous_and_balanced(built):
     rng = np.random.default_rng(0)
     for n, world in [(10, 3), (1, 4), (0, 2), (257, 8), (40, 1)]:
