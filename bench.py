@@ -102,8 +102,11 @@ def cpu_info() -> dict:
 
 
 def profile_summary(args) -> tuple[dict | None, str | None]:
+    def tag_order(q: Path):  # rNN then the revision letters: r02z < r02aa < r02ab
+        tag = q.name.split("_")[0]
+        return (tag[:3], len(tag), tag)
     cands = [Path(args.profile_summary)] if args.profile_summary else sorted(
-        (ROOT / "profiles").glob(f"r*_{args.config.lower()}_*summary.json"))  # round tags sort in order
+        (ROOT / "profiles").glob(f"r*_{args.config.lower()}_*summary.json"), key=tag_order)
     for q in reversed(cands):
         try:
             d = json.loads(q.read_text())
