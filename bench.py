@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--exchange", choices=("shm", "torch"), default="shm",
                     help="multi-process exchange: the library's shared-memory all-gather, or a torch.distributed "
                          "all-reduce callback")
+    ap.add_argument("--permute-mode", choices=("parity", "throughput"), default="parity",
+                    help="throughput: counter-based random numbers, trials independent (labelled non-parity)")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--chromosomes", type=int, default=None,
                     help="chromosomes (default: the config's; development aid)")
@@ -208,6 +210,8 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
+    fscl_amd.set_permute_mode(args.permute_mode)
+
     def job():
         fscl_amd.srand()  # every step is the same job (a fresh process's rand stream, fscl.c:135)
         fscl_amd.scan_chromosome(scan, tab)
@@ -278,7 +282,10 @@ def main() -> int:
         "data": "synthetic (seeded neutral-spectrum SNPs with planted sweeps, fscl_amd/synth.py)",
         "config": {"workload": f"{args.config}: {cfg['n_chr']} x ({cfg['snps_per_chr']} SNPs, "
                                f"{cfg['chr_len'] // 10**6} Mb, n={cfg['n']}) chromosome(s), G=100kb, "
-                               f"{n_permute} permutations, parity mode, one job split over {world} GPU(s)",
+                               f"{n_permute} permutations, "
+                               + ("parity mode" if args.permute_mode == "parity" else
+                                  "THROUGHPUT MODE (counter-based random numbers: non-parity, not the metric's mode)")
+                               + f", one job split over {world} GPU(s)",
                    "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"],
                    "units_per_step": units / args.steps, "exchange": args.exchange if world > 1 else None},
         "roofline": roof,

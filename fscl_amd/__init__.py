@@ -106,6 +106,7 @@ EXPORTS = [
     "fsclg_search_points", "fsclg_get_stats", "fsclg_reset_stats", "fsclg_interval_thresholds",
     "fsclg_row_buffer", "fsclg_slot_row_buffer", "fsclg_slot_set_rows", "fsclg_search_submit", "fsclg_search_wait",
     "fsclg_slot_windows", "ms_openfile", "ms_background", "ms_next_block",
+    "fscl_amd_set_permute_mode",
 ]
 
 
@@ -118,6 +119,7 @@ def _load() -> C.CDLL:
         "load_snp_input": (P(ScanT), [C.c_char_p, C.c_int, C.c_int]),
         "fscl_amd_load_ms_input": (P(ScanT), [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int]),
         "ms_openfile": (None, [C.c_char_p]),
+        "fscl_amd_set_permute_mode": (C.c_int, [C.c_int, C.c_ulonglong]),
         "ms_background": (P(ScanT), [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int]),
         "ms_next_block": (P(ScanT), [C.c_int, C.c_int, C.c_int, C.c_int]),
         "background_fsp": (P(P(C.c_double)), [P(ScanT), C.c_int, C.c_char_p, C.c_int]),
@@ -209,6 +211,16 @@ def ms_blocks(path, segment_length: int, folded: bool = False, sample_first: int
         if not s:
             return
         yield s
+
+
+PERMUTE_MODES = {"parity": 0, "throughput": 1}
+
+
+def set_permute_mode(mode: str = "parity", seed: int = 0xFD821A6) -> None:
+    """scan_permute's mode (include/fscl_amd.h): "parity" (the reference's rand() stream) or
+    "throughput" (counter-based random numbers from `seed`, labelled non-parity)."""
+    if get_lib().fscl_amd_set_permute_mode(PERMUTE_MODES[mode], int(seed)) != 0:
+        raise ValueError(mode)
 
 
 def background_fsp(scan, force_neutral: bool = False, bs_file=None, include_invariant: bool = False):
@@ -344,10 +356,12 @@ def shutdown() -> None:
 def run(snp_file=None, output=None, *, ms_file=None, ms_segment_length=0, ms_folded=False, n_permute=0,
         permute_nbp=0.1, asc_depth=0, asc_min_freq=1, ascbias_background_only=False, include_invariant=False,
         force_neutral=False, minimum_depth=5, large_grid_sp=100000, scan_width_mb=1.0, max_only=False,
-        label=None, eval_range=81920, bp_resl=128, verbosity=1):
+        label=None, eval_range=81920, bp_resl=128, verbosity=1, permute_mode="parity", permute_seed=0xFD821A6):
     """The fscl main() pipeline (fscl.c:316-337) in-process; returns the scan_t
-    pointer (points(scan) reads the results)."""
+    pointer (points(scan) reads the results).  permute_mode "throughput": the
+    counter-based permutation test (set_permute_mode)."""
     get_lib().configure_logmsg(int(verbosity))
+    set_permute_mode(permute_mode, permute_seed)
     init_log_table()
     srand()  # init_options (fscl.c:135): a fresh process's stream
     set_dump_output(output, label)

@@ -54,6 +54,7 @@ int main(int argc, char **argv) {
   int small_grid_sp = 1000, large_grid_sp = 100000, dont_scan = 0, minimum_obs_depth = 5, n_threads = 1;
   int verbosity = MSG_STATUS, eval_range = 81920, bp_resl = 128, stop = 0, i, n_gpus = 0;
   double permute_nbp = 0.1, alpha_factor = 1.0, scan_width_mb = 1.0;
+  char *permute_mode = NULL, *permute_seed = NULL;
   scan_t *s;
   double **fsp;
   opt_t opts[] = {
@@ -85,6 +86,9 @@ int main(int argc, char **argv) {
       {0, "no-scan", &dont_scan, T_FLAG, "do not scan chromosome, compute background frequency spectrum only"},
       {0, "ascbias-background-only", &bg_only, T_FLAG, "correct for ascertainment bias only in estimating the background site frequency spectrum"},
       {0, "n-gpus", &n_gpus, T_INT, "GPUs to use (default: every visible GPU, or $FSCL_AMD_DEVICE alone when set)"},
+      {0, "permute-mode", &permute_mode, T_STR, "parity (default: the reference's rand() stream, identical results) or "
+                                                "throughput (counter-based random numbers, trials independent; not identical)"},
+      {0, "permute-seed", &permute_seed, T_STR, "seed of the throughput mode's random numbers (default 0xFD821A6)"},
       {0, NULL, NULL, 0, NULL}};
 
   spline_pts = N_SPLINE_KNOTS;
@@ -165,6 +169,12 @@ int main(int argc, char **argv) {
   }
   if (large_grid_sp < 1) { logmsg(MSG_ERROR, "Error: coarse grid spacing must be positive.\n"); stop = 1; }
   if (n_gpus < 0) { logmsg(MSG_ERROR, "Error: --n-gpus must be >= 0.\n"); stop = 1; }
+  if (permute_mode && strcmp(permute_mode, "parity") && strcmp(permute_mode, "throughput")) {
+    logmsg(MSG_ERROR, "Error: --permute-mode must be parity or throughput.\n");
+    stop = 1;
+  }
+  if (permute_seed && !(permute_mode && !strcmp(permute_mode, "throughput")))
+    logmsg(MSG_WARN, "Warning: --permute-seed is used only with --permute-mode=throughput.\n");
   if (stop) {
     if (verbosity <= MSG_FATAL) logmsg(MSG_FATAL, "Fatal errors have occurred, use -v 1 or greater to see them.\n");
     exit(-1);
@@ -178,6 +188,10 @@ int main(int argc, char **argv) {
     sm_ptable_t *sm;
     if ((n_gpus > 0 || !getenv("FSCL_AMD_DEVICE")) && fscl_amd_set_devices(NULL, n_gpus) != 0)
       logmsg(MSG_FATAL, "fscl: --n-gpus=%d: at most 16 GPUs per process", n_gpus);
+    if (permute_mode && !strcmp(permute_mode, "throughput")) {
+      fscl_amd_set_permute_mode(FSCL_AMD_PERMUTE_THROUGHPUT, permute_seed ? strtoull(permute_seed, NULL, 0) : 0xFD821A6ull);
+      logmsg(MSG_STATUS, "permutation test in throughput mode (counter-based random numbers; not the reference's stream)\n");
+    }
     sm = compute_sweep_model_tables(s, fsp, asc_depth, asc_min_freq, bg_only, include_invariant);
     compute_snp_null_model(s, fsp);
     scan_chromosome(s, sm, eval_range, bp_resl, large_grid_sp, n_threads);

@@ -1325,6 +1325,276 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   free(g_pcost); g_pcost = NULL;
 }
 
+/* ------------------------------------------------ throughput mode (non-parity)
+   The reference's trials are serial because one rand() stream feeds every permutation and
+   every prune draw (scan-chromosome.c:441-456, 488-498).  In throughput mode the randomness
+   is counter-based instead, so no trial depends on another:
+     * trial t's permutation is block_permute driven by its own generator, the glibc TYPE_3
+       stream seeded with tp_trial_seed(seed, t);
+     * point i's prune draw in trial t is tp_prune_rand(seed, t, i);
+     * a point's results are applied in trial order (hits, the p >= 20 prune test with the
+       pre-increment count, the saved null CLRs) and it stops at its first prune, exactly as
+       in the reference; results of later trials that were already evaluated are dropped.
+   Each point's outcome is then a function of (seed, point) alone: identical for any number
+   of GPUs, ranks, trials in flight or worker threads, and restated by the oracle
+   (--throughput-seed).  Not bit-identical to the reference (different random numbers), but
+   the same procedure: every trial is an independent block permutation, so the p-values have
+   the reference's distribution.
+   Schedule: rounds of Q = world * n_dev trials, trial r*Q + rank*n_dev + l on local device l;
+   up to K rounds in flight (one row slot and one batch per round and device); round r
+   evaluates the points still active after every round <= r - K is applied.  Worker threads
+   build the permutations (and whole-chromosome null sums) of the next trials ahead, in any
+   order, into a ring of pinned buffers. */
+static int g_pmode = FSCL_AMD_PERMUTE_PARITY;
+static unsigned long long g_pseed = 0xFD821A6ull;
+
+int fscl_amd_set_permute_mode(int mode, unsigned long long seed) {
+  if (mode != FSCL_AMD_PERMUTE_PARITY && mode != FSCL_AMD_PERMUTE_THROUGHPUT) return -1;
+  g_pmode = mode;
+  g_pseed = seed;
+  return 0;
+}
+
+static uint64_t mix64(uint64_t z) { /* splitmix64's output function */
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static unsigned tp_trial_seed(uint64_t seed, long t) { return (unsigned)(mix64(seed ^ mix64((uint64_t)t + 1)) >> 32); }
+static int tp_prune_rand(uint64_t seed, long t, int i) { /* 31 bits, as rand() */
+  return (int)(mix64(mix64(seed ^ 0x632BE59BD9B4E019ull) ^ ((uint64_t)(uint32_t)t << 32 | (uint32_t)i)) >> 33);
+}
+
+static struct {
+  pthread_t th[SPEC_MAX];
+  int n_th;
+  pthread_mutex_t mu;
+  pthread_cond_t cv, done;
+  int stop;
+  long next, limit, total;  /* local trials j: the next to build; build only j < limit, j < total */
+  int nb;                   /* ring of buffers: trial j in buf[j % nb] */
+  uint32_t **buf;
+  double **nul;
+  long *built;              /* the trial each buffer holds, -1 none */
+  long q, rank_off, n_perm; /* local trial j -> global trial (j / n_dev) * q + rank_off + j % n_dev */
+  int n_dev;
+  const snp_t *snps;
+  int n;
+  double nbp, width_mb;
+  unsigned long long negj;
+  double gen_s;
+} TB = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
+
+static long tb_trial(long j) { return j / TB.n_dev * TB.q + TB.rank_off + j % TB.n_dev; }
+
+static void tb_build(long j) {
+  static const unsigned zero = 0;
+  const int b = (int)(j % TB.nb);
+  const long t = tb_trial(j);
+  unsigned long long negj = 0;
+  if (t <= TB.n_perm) {
+    fh_rand_t g;
+    fh_srand(&g, tp_trial_seed(g_pseed, t));
+    block_permute(TB.buf[b], D.row, TB.snps, TB.n, TB.nbp, TB.width_mb, &g, &negj, NULL, 0);
+    chr_null_sums_1t(TB.buf[b], TB.nul[b], &zero, 0);
+  }
+  pthread_mutex_lock(&TB.mu);
+  TB.negj += negj;
+  TB.built[b] = j;
+  pthread_cond_broadcast(&TB.done);
+  pthread_mutex_unlock(&TB.mu);
+}
+
+static void *tb_worker(void *arg) {
+  (void)arg;
+  pthread_mutex_lock(&TB.mu);
+  for (;;) {
+    while (!TB.stop && !(TB.next < TB.limit && TB.next < TB.total)) pthread_cond_wait(&TB.cv, &TB.mu);
+    if (TB.stop) break;
+    {
+      const long j = TB.next++;
+      double t0;
+      pthread_mutex_unlock(&TB.mu);
+      t0 = fh_now();
+      tb_build(j);
+      pthread_mutex_lock(&TB.mu);
+      TB.gen_s += fh_now() - t0;
+    }
+  }
+  pthread_mutex_unlock(&TB.mu);
+  return NULL;
+}
+
+/* trial j's buffer index, once it is built (by the main thread when there are no workers) */
+static int tb_get(long j) {
+  const int b = (int)(j % TB.nb);
+  if (TB.n_th == 0) {
+    if (TB.built[b] != j) tb_build(j);
+    return b;
+  }
+  pthread_mutex_lock(&TB.mu);
+  while (TB.built[b] != j) pthread_cond_wait(&TB.done, &TB.mu);
+  pthread_mutex_unlock(&TB.mu);
+  return b;
+}
+
+/* every trial below j has been read by its upload: their buffers may take later trials */
+static void tb_release(long j) {
+  pthread_mutex_lock(&TB.mu);
+  if (j + TB.nb > TB.limit) TB.limit = j + TB.nb;
+  pthread_cond_broadcast(&TB.cv);
+  pthread_mutex_unlock(&TB.mu);
+}
+
+static void tb_stop(void) {
+  int t;
+  pthread_mutex_lock(&TB.mu);
+  TB.stop = 1;
+  pthread_cond_broadcast(&TB.cv);
+  pthread_mutex_unlock(&TB.mu);
+  for (t = 0; t < TB.n_th; t++) pthread_join(TB.th[t], NULL);
+  for (t = 0; t < TB.nb; t++) { fsclg_host_free(TB.buf[t]); free(TB.nul[t]); }
+  free(TB.buf); free(TB.nul); free(TB.built);
+  TB.buf = NULL; TB.nul = NULL; TB.built = NULL;
+  TB.n_th = TB.nb = 0;
+  TB.stop = 0;
+}
+
+typedef struct {
+  long r;
+  int n, cap;
+  int *pt;               /* the round's active points, ascending */
+  fsclg_cell_t *cells;   /* their G-aligned cells (Q5), the same for every trial of the round */
+  fsclg_point_t *out;    /* [Q][n]: trial q of the round at out + q * n */
+  size_t out_cap;
+  int live[FH_MAX_DEV];  /* local device l submitted its trial */
+} tp_round_t;
+
+static void permute_throughput(scan_t *s, int n_perm, double permute_nbp, int eval_range, int bp_resl,
+                               int large_grid_sp, double scan_width_mb, int save) {
+  /* rounds in flight: about 8 trials in all (at least 2 rounds), so that a pruned point's
+     evaluations past its prune stay few; FSCL_AMD_DEPTH overrides */
+  const char *env = getenv("FSCL_AMD_DEPTH");
+  const int nd = D.n_dev, Q = D.world * nd;
+  const int K = env ? (atoi(env) < 1 ? 1 : (atoi(env) > FSCLG_N_SLOTS ? FSCLG_N_SLOTS : atoi(env)))
+                    : (Q >= 4 ? 2 : FSCLG_N_SLOTS / Q);
+  const long R = ((long)n_perm + Q) / Q; /* rounds holding trials 0 .. n_perm */
+  tp_round_t rd[FSCLG_N_SLOTS];
+  long r_sub = 0, r_done = 0;
+  int stop_sub = 0, i, k, l;
+  memset(rd, 0, sizeof rd);
+  /* the builders: one ring buffer per trial in flight and per worker, plus a round ahead */
+  TB.n_dev = nd; TB.q = Q; TB.rank_off = (long)D.rank * nd; TB.n_perm = n_perm;
+  TB.snps = s->snps; TB.n = s->n_snps; TB.nbp = permute_nbp; TB.width_mb = scan_width_mb;
+  TB.total = R * nd; TB.next = 0; TB.negj = 0; TB.gen_s = 0.;
+  {
+    const int want = spec_threads_wanted();
+    TB.nb = (K + 1) * nd + want;
+    TB.limit = TB.nb;
+    TB.buf = fh_calloc((size_t)TB.nb, sizeof(uint32_t *), "permutation ring");
+    TB.nul = fh_calloc((size_t)TB.nb, sizeof(double *), "permutation ring");
+    TB.built = fh_malloc(sizeof(long) * (size_t)TB.nb, "permutation ring");
+    for (i = 0; i < TB.nb; i++) {
+      TB.buf[i] = fsclg_host_alloc(sizeof(uint32_t) * (size_t)(s->n_snps ? s->n_snps : 1));
+      if (!TB.buf[i]) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
+      TB.nul[i] = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
+      TB.built[i] = -1;
+    }
+    for (TB.n_th = 0; TB.n_th < want; TB.n_th++)
+      if (pthread_create(&TB.th[TB.n_th], NULL, tb_worker, NULL) != 0) break;
+    D.st.spec_threads = TB.n_th;
+  }
+  while (r_done < r_sub || (!stop_sub && r_sub < R)) {
+    if (!stop_sub && r_sub < R && r_sub - r_done < K) {
+      tp_round_t *b = rd + r_sub % K;
+      const int slot = (int)(r_sub % K);
+      double tp = fh_now();
+      b->n = 0;
+      if (b->cap < s->n_scan_pts) {
+        b->cap = s->n_scan_pts;
+        b->pt = fh_realloc(b->pt, sizeof(int) * (size_t)(b->cap ? b->cap : 1), "round");
+        b->cells = fh_realloc(b->cells, sizeof(fsclg_cell_t) * (size_t)(b->cap ? b->cap : 1), "round");
+      }
+      for (i = 0; i < s->n_scan_pts; i++) {
+        const scan_pt_t *q = s->scan_pts + i;
+        fsclg_cell_t *cl = b->cells + b->n;
+        if (q->permute_finished) continue;
+        cl->chr = q->chr;
+        cl->start_pos = q->sweep_pos - (q->sweep_pos % large_grid_sp); /* Q5: G-aligned, unclipped */
+        cl->end_pos = cl->start_pos + large_grid_sp;
+        cl->pad = 0;
+        b->pt[b->n++] = i;
+      }
+      if (b->n == 0) { stop_sub = 1; continue; }
+      if (b->out_cap < (size_t)Q * b->n) {
+        b->out_cap = (size_t)Q * b->n;
+        b->out = fh_realloc(b->out, sizeof(fsclg_point_t) * b->out_cap, "round");
+      }
+      b->r = r_sub;
+      cr_logmsg(MSG_STATUS, "Scanning snp block permutations... %7ld (%d scan pts remaining)        ", r_sub * Q, b->n);
+      for (l = 0; l < nd; l++) {
+        const long j = r_sub * nd + l;
+        int bi;
+        b->live[l] = tb_trial(j) <= n_perm;
+        if (!b->live[l]) continue;
+        tp = fh_now();
+        bi = tb_get(j);
+        D.st.host_perm_s += fh_now() - tp;
+        tp = fh_now();
+        dev_check(fsclg_slot_set_rows_host(D.ctx[l], slot, TB.buf[bi], TB.nul[bi]), "set rows");
+        D.st.host_upload_s += fh_now() - tp;
+        dev_check(fsclg_slot_windows(D.ctx[l], slot, b->cells, b->n, eval_range), "window sums");
+        dev_check(fsclg_search_submit(D.ctx[l], 2 + slot, slot, b->cells, b->n, eval_range, bp_resl), "search submit");
+        D.st.gp_evals += (unsigned long long)b->n;
+      }
+      r_sub++;
+    } else {
+      tp_round_t *b = rd + r_done % K;
+      const int lo = D.rank * nd;
+      double tw = fh_now();
+      for (l = 0; l < nd; l++)
+        if (b->live[l])
+          dev_check(fsclg_search_wait(D.ctx[l], 2 + (int)(r_done % K), b->out + (size_t)(lo + l) * b->n), "search wait");
+        else
+          memset(b->out + (size_t)(lo + l) * b->n, 0, sizeof(fsclg_point_t) * (size_t)b->n);
+      D.st.wait_s += fh_now() - tw;
+      exchange_points(b->out, Q * b->n, lo * b->n, (lo + nd) * b->n);
+      tb_release((r_done + 1) * nd); /* the round's uploads ran before its searches */
+      tw = fh_now();
+      for (k = 0; k < Q; k++) { /* the round's trials in order, each point in ascending order */
+        const long t = r_done * Q + k;
+        const fsclg_point_t *o = b->out + (size_t)k * b->n;
+        int any = 0;
+        if (t > n_perm) break;
+        for (i = 0; i < b->n; i++) {
+          scan_pt_t *p = s->scan_pts + b->pt[i];
+          const double clr = o[i].clr;
+          if (p->permute_finished) continue; /* pruned in an earlier trial: later results dropped */
+          any = 1;
+          if (clr >= p->clr) {
+            p->permute_p++;
+            if (p->permute_p >= 20 && p->permute_p / (double)p->permute_n >= tp_prune_rand(g_pseed, t, b->pt[i]) / (2147483647 + 1.0))
+              p->permute_finished = 1; /* Q7: ratio uses the pre-increment count */
+          }
+          if (p->permute_n < save) p->permute_clr[p->permute_n] = (float)clr;
+          p->permute_n++;
+          if (clr < 0 || clr > 1000000 || isnan(clr))
+            fprintf(stderr, "%d\t%d\t%g\t%1.3e\n", p->chr, b->cells[i].start_pos, clr, exp(o[i].lalpha));
+        }
+        D.st.trials += any;
+      }
+      D.st.prune_s += fh_now() - tw;
+      r_done++;
+      if (g_sigint) sigint_dump(s, n_perm); /* every trial applied so far */
+    }
+  }
+  D.st.negj += TB.negj;
+  D.st.spec_gen_s += TB.gen_s;
+  tb_stop();
+  for (k = 0; k < FSCLG_N_SLOTS; k++) { free(rd[k].pt); free(rd[k].cells); free(rd[k].out); }
+}
+
 /* scan-chromosome.c:582-652 (with --n-threads=1 pruning semantics) */
 void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, double alpha_factor, int n_threads,
                   int eval_range, int bp_resl, int large_grid_sp, double scan_width_mb) {
@@ -1347,9 +1617,18 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   sigemptyset(&sa.sa_mask);
   gettimeofday(&g_last_dump, NULL);
   sigaction(SIGINT, &sa, NULL);
-  (void)fh_rand(g); /* scan-chromosome.c:440: the single thread's usleep() draw */
   for (i = 0; i < s->n_scan_pts; i++) /* points a caller built without scan_chromosome */
     if (!s->scan_pts[i].permute_clr) s->scan_pts[i].permute_clr = fh_malloc(sizeof(float) * save, "permute_clr");
+  {
+    const char *e = getenv("FSCL_AMD_PERMUTE"); /* throughput[:seed] overrides the mode set by the API */
+    if (e && !strncmp(e, "throughput", 10)) fscl_amd_set_permute_mode(FSCL_AMD_PERMUTE_THROUGHPUT,
+                                                                       e[10] == ':' ? strtoull(e + 11, NULL, 0) : g_pseed);
+  }
+  if (g_pmode == FSCL_AMD_PERMUTE_THROUGHPUT) { /* the rand() stream is not used */
+    permute_throughput(s, n_perm, permute_nbp, eval_range, bp_resl, large_grid_sp, scan_width_mb, save);
+    goto done;
+  }
+  (void)fh_rand(g); /* scan-chromosome.c:440: the single thread's usleep() draw */
   if (!getenv("FSCL_AMD_LOCKSTEP")) {
     permute_pipelined(s, n_perm, permute_nbp, eval_range, bp_resl, large_grid_sp, scan_width_mb, g, save);
     goto done;

@@ -154,6 +154,18 @@ scan_t *fscl_amd_load_ms_input(const char *ms_fname, int segment_length, int ms_
    fscl_amd_srand restarts it (what a fresh process would see). */
 void fscl_amd_srand(unsigned seed);
 
+/* permutation mode of scan_permute.  FSCL_AMD_PERMUTE_PARITY (default): the reference's
+   procedure on its rand() stream, results identical to the reference.
+   FSCL_AMD_PERMUTE_THROUGHPUT (labelled non-parity): the same procedure with
+   counter-based random numbers -- trial t's block permutation from the glibc stream seeded by a
+   hash of (seed, t), point i's prune draw in trial t a hash of (seed, t, i) -- so trials run
+   independently on every GPU and rank; results are a function of the seed alone (any number of
+   GPUs), and match the oracle's --throughput-seed.  $FSCL_AMD_PERMUTE=throughput[:seed]
+   overrides.  Returns 0, or -1 for an unknown mode. */
+#define FSCL_AMD_PERMUTE_PARITY 0
+#define FSCL_AMD_PERMUTE_THROUGHPUT 1
+int fscl_amd_set_permute_mode(int mode, unsigned long long seed);
+
 /* what a SIGINT during scan_permute writes (scan-chromosome.c:553-560): by default
    fscl.c's globals output_fname / prepend_label; a library caller sets them here */
 void fscl_amd_set_dump_output(const char *fname, const char *label);

@@ -784,6 +784,22 @@ static orc_rand_t g_rng;
 static int g_rng_seeded = 0;
 void orc_reseed(unsigned seed) { orc_srand(&g_rng, seed); g_rng_seeded = 1; }
 
+/* The product's throughput mode (include/fscl_amd.h, fscl_amd_set_permute_mode; DESIGN.md
+   §5.4) restated serially: the reference's trial loop and prune test above, with trial t's
+   permutation drawn from the glibc stream seeded by orc_tp_trial_seed(seed, t) and point i's
+   prune draw in trial t = orc_tp_prune_rand(seed, t, i).  Not the reference's stream, so this
+   pins the product's own non-parity mode (its definition, not the reference's numbers). */
+static uint64_t orc_mix64(uint64_t z) { /* splitmix64 output function */
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static unsigned orc_tp_trial_seed(uint64_t seed, long t) { return (unsigned)(orc_mix64(seed ^ orc_mix64((uint64_t)t + 1)) >> 32); }
+static int orc_tp_prune_rand(uint64_t seed, long t, int i) {
+  return (int)(orc_mix64(orc_mix64(seed ^ 0x632BE59BD9B4E019ull) ^ ((uint64_t)(uint32_t)t << 32 | (uint32_t)i)) >> 33);
+}
+
 void orc_scan_permute(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t *o, orc_stats_t *st) {
   orc_rand_t *const gp = &g_rng;
   orc_snp_t *ps = xmalloc(sizeof(orc_snp_t) * s->n_snps);
@@ -792,13 +808,19 @@ void orc_scan_permute(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t *o
   const int save = CLR_NULL_DIST_SAVE; /* scan-chromosome.c:240,496 */
   orc_stats_t tot = {0};
   if (!g_rng_seeded) orc_reseed(0xFD821A6);
-  (void)orc_rand(gp);       /* scan-chromosome.c:440: the usleep() draw of the one thread */
+  if (!o->throughput) (void)orc_rand(gp); /* scan-chromosome.c:440: the usleep() draw of the one thread */
   for (i = 0; i < s->n_pts; i++) {
     act[i] = i;
     if (!s->pts[i].permute_clr) s->pts[i].permute_clr = xmalloc(sizeof(float) * CLR_NULL_DIST_SAVE);
   }
   for (;;) {
-    orc_block_permute(ps, s->snps, s->n_snps, o->permute_nbp, o->scan_width_mb, gp, &tot);
+    if (o->throughput) { /* trial + 1's own stream (nothing else draws from it) */
+      orc_rand_t tg;
+      orc_srand(&tg, orc_tp_trial_seed(o->throughput_seed, trial + 1));
+      orc_block_permute(ps, s->snps, s->n_snps, o->permute_nbp, o->scan_width_mb, &tg, &tot);
+    } else {
+      orc_block_permute(ps, s->snps, s->n_snps, o->permute_nbp, o->scan_width_mb, gp, &tot);
+    }
     trial++;
     for (i = k = 0; i < n_act; i++)
       if (!s->pts[act[i]].permute_finished) act[k++] = act[i];
@@ -822,7 +844,9 @@ void orc_scan_permute(orc_scan_t *s, const orc_table_t *tab, const orc_opts_t *o
       orc_pt_t *q = s->pts + act[i];
       if (clr[i] >= q->clr) {
         q->permute_p++;
-        if (q->permute_p >= 20 && q->permute_p / (double)q->permute_n >= orc_rand(gp) / (2147483647 + 1.0))
+        if (q->permute_p >= 20 &&
+            q->permute_p / (double)q->permute_n >=
+                (o->throughput ? orc_tp_prune_rand(o->throughput_seed, trial, act[i]) : orc_rand(gp)) / (2147483647 + 1.0))
           q->permute_finished = 1; /* Q7 */
       }
       if (q->permute_n < save) q->permute_clr[q->permute_n] = (float)clr[i];

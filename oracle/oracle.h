@@ -100,6 +100,8 @@ typedef struct {
   int bp_resl;          /* fscl.c:174 */
   int max_only;
   int n_threads;        /* OpenMP threads for the lockstep-parallel port (results identical) */
+  int throughput;       /* the product's throughput mode (counter-based random numbers) */
+  unsigned long long throughput_seed;
 } orc_opts_t;
 
 /* counters used for the algorithmic-bytes roofline */

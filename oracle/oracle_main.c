@@ -19,6 +19,7 @@ int main(int argc, char **argv) {
   orc_opts_t o;
   char *snp = NULL, *out = NULL, *label = NULL, *ms = NULL, *bs = NULL, *obs = NULL, *dump = NULL;
   int small_grid = 1000, verbosity = 3, no_scan = 0, dummy_i = 0, stop = 0, i, ms_folded = 0, nulldist = 0;
+  char *tseed = NULL;
   double alpha_factor = 1.0;
   orc_stats_t st = {0};
   orc_default_opts(&o);
@@ -54,6 +55,7 @@ int main(int argc, char **argv) {
         {0, "dump-points", &dump, T_STR}, /* oracle only: hex-float dump of every point */
         {0, "nulldist", &nulldist, T_FLAG}, /* oracle only: write <output>-nulldist at the end */
         {0, "eval-range", &o.eval_range, T_INT}, /* oracle only: scan_chromosome's eval_range (fscl.c:175 fixes 81920) */
+        {0, "throughput-seed", &tseed, T_STR}, /* oracle only: the product's throughput permutation mode */
         {0, NULL, NULL, 0}};
     i = 1;
     while (i < argc) {
@@ -95,6 +97,7 @@ int main(int argc, char **argv) {
   }
   if (ms || bs || obs || no_scan) { fprintf(stderr, "oracle: -m/-b/--output-bs/--no-scan not restated\n"); stop = 1; }
   if (stop) return 255;
+  if (tseed) { o.throughput = 1; o.throughput_seed = strtoull(tseed, NULL, 0); }
   if (dump) setenv("ORC_DUMP_POINTS", dump, 1);
   if (nulldist) setenv("ORC_NULLDIST", "1", 1);
   if (orc_run_snpfile(snp, out, &o, label, &st) != 0) return 1;

@@ -503,3 +503,71 @@ def test_sigint_dumps_table_and_null_distribution(built, tmp):
     run_oracle(snp, tmp / "o.txt", ["--coarse-grid-spacing=60000", f"--n-permute={n_trials - 1}", "--nulldist"])
     assert out.read_text() == (tmp / "o.txt").read_text()
     assert (tmp / "g.txt-nulldist").read_text() == (tmp / "o.txt-nulldist").read_text()
+
+
+# ---------------------------------------------------------------- throughput mode
+TP_SEED = 0x5EED1234
+
+
+@pytest.fixture(scope="module")
+def tp_case(tmp_path_factory):
+    """Enough trials that points reach permute_p >= 20 and are pruned in throughput mode; the
+    oracle's serial restatement of the mode (--throughput-seed) is the reference result."""
+    d = tmp_path_factory.mktemp("tp")
+    snp = d / "tp.snp"
+    synth.write_snp_file(str(snp), synth.generate(n_chr=3, chr_len=5_000_000, snps_per_chr=5000, n=30, seed=97,
+                                                  sweeps_per_chr=1))
+    opts = ["--coarse-grid-spacing=40000", "--n-permute=60"]
+    run_oracle(snp, d / "o.txt", [*opts, f"--throughput-seed={TP_SEED}"], d / "o.dump")
+    return snp, opts, read_dump(d / "o.dump"), (d / "o.txt").read_text()
+
+
+@pytest.mark.parametrize("depth", ["8", "3", "1"])
+def test_throughput_mode_matches_oracle(built, tmp, tp_case, monkeypatch, depth):
+    """Throughput mode (include/fscl_amd.h fscl_amd_set_permute_mode):
+    counter-based random numbers, trials independent.  Its results are a function of the seed
+    alone -- the same with 8, 3 or 1 rounds in flight -- and equal the oracle's restatement of
+    the mode bit for bit, with pruning exercised."""
+    snp, opts, want, want_out = tp_case
+    monkeypatch.setenv("FSCL_AMD_DEPTH", depth)
+    fscl_amd.reset_stats()
+    scan = fscl_amd.run(snp, tmp / "g.txt", permute_mode="throughput", permute_seed=TP_SEED, **_kw(opts))
+    pts = fscl_amd.points(scan)
+    assert (pts["permute_n"] < 61).any() and (pts["permute_n"] == 61).any()  # pruned and surviving points
+    assert_rows_equal(points_rows(pts), want, f"throughput depth {depth}")
+    assert (tmp / "g.txt").read_text() == want_out
+    fscl_amd.set_permute_mode("parity")
+
+
+def test_throughput_mode_two_devices_and_cli(built, tmp, tp_case):
+    """Throughput mode shards whole trials over devices (two contexts on GPU 0 here) and over
+    ranks; the CLI's --permute-mode=throughput --permute-seed gives the same output."""
+    snp, opts, want, want_out = tp_case
+    fscl_amd.set_devices([0, 0])
+    try:
+        scan = fscl_amd.run(snp, tmp / "g.txt", permute_mode="throughput", permute_seed=TP_SEED, **_kw(opts))
+        assert fscl_amd.get_lib().fscl_amd_n_devices() == 2
+        assert_rows_equal(points_rows(fscl_amd.points(scan)), want, "throughput, two devices")
+    finally:
+        fscl_amd.set_device(0)
+        fscl_amd.set_permute_mode("parity")
+    r = subprocess.run([str(CLI), "-f", str(snp), "-o", str(tmp / "c.txt"), "--permute-mode=throughput",
+                        f"--permute-seed={TP_SEED}", *opts], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert (tmp / "c.txt").read_text() == want_out
+
+
+def test_throughput_mode_two_ranks(built, tmp, tp_case):
+    """Two processes on GPU 0, shared-memory exchange: each rank runs every other trial."""
+    snp, opts, want, want_out = tp_case
+    env = dict(os.environ, WORLD_SIZE="2", FSCL_AMD_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               FSCL_AMD_RANK_TIMEOUT="120", FSCL_MR_SHM=f"/fscl_amd_tp_{os.getpid()}",
+               FSCL_AMD_PERMUTE=f"throughput:{TP_SEED}", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(29600 + os.getpid() % 1000))
+    procs = [subprocess.Popen([sys.executable, str(ROOT / "tests" / "mr_worker.py"), str(snp), str(tmp / f"o{r}.txt"),
+                               *opts], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for r in range(2)]
+    for p in procs:
+        out, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err
+    assert (tmp / "o0.txt").read_text() == want_out

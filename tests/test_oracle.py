@@ -34,6 +34,26 @@ def test_oracle_threads_do_not_change_results(built, tmp):
     assert (tmp / "a.dump").read_bytes() == (tmp / "b.dump").read_bytes()
 
 
+def test_throughput_mode_restatement(built, tmp):
+    """The oracle's restatement of the product's throughput mode (--throughput-seed): thread
+    count does not change it, another seed does, and its permutation counts follow the
+    reference's procedure (N+1 trials for surviving points; a pruned point stopped at a hit
+    with permute_p >= 20)."""
+    c = manifest()["cases"]["g1_p25"]
+    snp = GOLD / c["input"]
+    opts = ["--n-permute=60"]
+    run_oracle(snp, tmp / "a", [*opts, "--throughput-seed=7"], tmp / "a.dump", threads=1)
+    run_oracle(snp, tmp / "b", [*opts, "--throughput-seed=7"], tmp / "b.dump", threads=4)
+    run_oracle(snp, tmp / "c", [*opts, "--throughput-seed=8"], tmp / "c.dump", threads=4)
+    assert (tmp / "a.dump").read_bytes() == (tmp / "b.dump").read_bytes()
+    assert (tmp / "a.dump").read_bytes() != (tmp / "c.dump").read_bytes()
+    rows = read_dump(tmp / "a.dump")
+    for r in rows:
+        p, n, fin = r[9], r[10], r[11]
+        assert (n == 61 and not fin) or (fin and p >= 20 and n < 61) or (fin and n == 61)
+    assert any(r[11] for r in rows)
+
+
 def _glibc_stream(seed: int, n: int) -> list[int]:
     libc = C.CDLL("libc.so.6")
     libc.srand(seed)
