@@ -1273,8 +1273,11 @@ __device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
     }
     __syncthreads();
     if (tid == 0) S.cnt[1] += (unsigned long long)S.pt[0].n_snps;
-    search_maxalpha_pts<LDS>(S, P, 0, 1);
-    if (tid == 0) write_point(P.out[cell], S.pt[0]);
+    search_maxalpha_pts<LDS, SPLIT>(S, P, 0, 1);  // split: the point's walks dealt over the members
+    if (tid == 0 && member == 0) {
+      S.pt[0].flags |= S.xfail;
+      write_point(P.out[cell], S.pt[0]);
+    }
   } else if (P.mode == 2) {
     // distinct cell endpoints, two per block: scan-chromosome.c:130-134 for each
     const int e0 = 2 * cell, np = min(2, P.n_ep - e0);
@@ -2622,11 +2625,38 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
   HIPCHK(hipStreamWaitEvent(B.stream, c->slot[0].ready, 0), "hipStreamWaitEvent");
   memcpy(B.p_out, pts, sizeof(fsclg_point_t) * n_pts);  // read and written in place by the kernel
   Params P = make_params(c, B, 0, n_pts, 1, 0, 0);
+  // latency (the reference's scan loop calls search_maxalpha once per point): a few points get
+  // up to FSCLG_POINTS_SPLIT workgroups each (default 8), which share every walk's segments as
+  // a split cell's members do
+  static const int psplit = getenv("FSCLG_POINTS_SPLIT") ? atoi(getenv("FSCLG_POINTS_SPLIT")) : 8;
+  int G = std::min(std::min(psplit, MAXSPLIT), 256 / n_pts);
+  if (G < 2) G = 1;
+  if (G > 1) {
+    const int nl = (n_pts + 7) / 8 * 8;
+    const size_t xb = (size_t)nl * 2 * sizeof(XAcc);
+    if (B.xacc_cap < xb) {
+      if (B.d_xacc) hipFree(B.d_xacc);
+      B.d_xacc = nullptr; B.xacc_cap = 0;
+      HIPCHK(hipMalloc((void**)&B.d_xacc, xb), "hipMalloc split accumulators");
+      B.xacc_cap = xb;
+    }
+    if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, nl))) return r;
+    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");
+    P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
+    P.ivc0 = 0; P.n_civ = 0; P.civ_max = 0; P.n_cache = 0;  // as a split batch: no LDS coefficient windows
+    P.off_thr = 0; P.off_nul = (c->n_iv + 1) * 8;
+    P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8;
+  }
   HIPCHK(hipEventRecord(B.ev0, B.stream), "hipEventRecord");
-  if ((r = launch_blocks(B.stream, P, n_pts))) return r;
+  if ((r = launch_blocks(B.stream, P, G > 1 ? (n_pts + 7) / 8 * 8 * G : n_pts))) return r;
   HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
   HIPCHK(hipEventSynchronize(B.ev1), "hipEventSynchronize");
   memcpy(pts, B.p_out, sizeof(fsclg_point_t) * n_pts);
+  for (int i = 0; i < n_pts; i++)
+    if (pts[i].flags & (PF_UNSUPPORTED | PF_SPLIT_TIMEOUT))
+      return set_err(pts[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL,
+                     pts[i].flags & PF_SPLIT_TIMEOUT ? "device flag: a point's members were not resident together"
+                                                     : "device flag");
   float ms = 0.f, t0 = 0.f, t1 = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, B.ev0, B.ev1), "hipEventElapsedTime");
   HIPCHK(hipEventElapsedTime(&t0, c->ev_ref, B.ev0), "hipEventElapsedTime");

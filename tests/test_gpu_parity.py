@@ -194,9 +194,10 @@ def test_ms_block_loop_matches_whole_file(built, tmp):
 def test_search_maxalpha_dropin(built):
     """search_maxalpha() on caller-initialised points (the reference's own scan loop calls it per
     point, scan-chromosome.c:126-135) equals the golden points, every one of them.  Its tables
-    and sites stay resident between calls, so a call costs one alpha search's latency on the
-    GPU (about 0.2 ms), not a re-upload: bounded here at 1 ms per call.  The per-point loop
-    stays slower than one scan_chromosome, which runs all the cells' bisections at once."""
+    and sites stay resident between calls, and each call spreads its point over up to 8
+    workgroups: a call costs one alpha search's latency on the GPU (about 85 us), not a
+    re-upload; bounded here at 1 ms per call.  The per-point loop stays slower than one
+    scan_chromosome (2.4x on the box), which runs every cell's bisection at once."""
     import ctypes as C
     import time
     case = "g2_p30"
