@@ -186,7 +186,20 @@ int main(int argc, char **argv) {
   if (output_bs_fname) output_background_fs(output_bs_fname, s, fsp);
   if (!dont_scan) {
     sm_ptable_t *sm;
-    if ((n_gpus > 0 || !getenv("FSCL_AMD_DEVICE")) && fscl_amd_set_devices(NULL, n_gpus) != 0)
+    const char *ws = getenv("WORLD_SIZE"), *rk = getenv("RANK");
+    if (ws && rk && atoi(ws) > 1) {
+      /* one process per GPU (e.g. under torch.distributed.run): GPU $LOCAL_RANK (or
+         $FSCL_AMD_DEVICE), results exchanged through a shared-memory segment named by
+         $FSCL_AMD_SHM_NAME, else the launcher's run id or port; rank 0 writes the output */
+      const char *id = getenv("FSCL_AMD_SHM_NAME");
+      char name[160];
+      if (!id) id = getenv("TORCHELASTIC_RUN_ID");
+      if (!id) id = getenv("MASTER_PORT");
+      snprintf(name, sizeof name, "/fscl_amd_%s", id ? id : "job");
+      if (n_gpus > 1) logmsg(MSG_WARN, "Warning: --n-gpus is ignored with one process per GPU (WORLD_SIZE=%s).\n", ws);
+      if (fscl_amd_set_ranks_shm(atoi(rk), atoi(ws), name) != 0)
+        logmsg(MSG_FATAL, "fscl: rank %s of %s could not meet the other ranks (%s)", rk, ws, name);
+    } else if ((n_gpus > 0 || !getenv("FSCL_AMD_DEVICE")) && fscl_amd_set_devices(NULL, n_gpus) != 0)
       logmsg(MSG_FATAL, "fscl: --n-gpus=%d: at most 16 GPUs per process", n_gpus);
     if (permute_mode && !strcmp(permute_mode, "throughput")) {
       fscl_amd_set_permute_mode(FSCL_AMD_PERMUTE_THROUGHPUT, permute_seed ? strtoull(permute_seed, NULL, 0) : 0xFD821A6ull);

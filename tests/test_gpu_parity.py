@@ -384,6 +384,21 @@ def test_two_devices_in_one_process_match_oracle(built, tmp, two_contexts, name,
     assert fscl_amd.get_stats()["n_devices"] == 2
 
 
+def test_cli_one_process_per_gpu(built, tmp):
+    """The CLI under a one-process-per-GPU launcher (RANK / WORLD_SIZE in the environment):
+    two ranks on GPU 0 exchange through shared memory; rank 0 writes the golden output."""
+    c = manifest()["cases"]["g1_p25"]
+    env = dict(os.environ, WORLD_SIZE="2", FSCL_AMD_DEVICE="0", FSCL_AMD_SHM_NAME=f"cli_{os.getpid()}",
+               FSCL_AMD_RANK_TIMEOUT="120")
+    procs = [subprocess.Popen([str(CLI), "-f", str(GOLD / c["input"]), "-o", str(tmp / "o.txt"), *c["options"]],
+                              env=dict(env, RANK=str(r), LOCAL_RANK="0"), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    for p in procs:
+        out, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err
+    assert (tmp / "o.txt").read_text() == (GOLD / "g1_p25.out").read_text()
+
+
 def test_cli_n_gpus(built, tmp):
     """fscl --n-gpus=1 and the CLI's default (every visible GPU) reproduce the golden output."""
     c = manifest()["cases"]["g1_p25"]
