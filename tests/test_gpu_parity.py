@@ -573,6 +573,25 @@ def test_throughput_mode_two_devices_and_cli(built, tmp, tp_case):
     assert (tmp / "c.txt").read_text() == want_out
 
 
+def test_throughput_mode_windowed_matches_oracle(built, tmp):
+    """Throughput mode on chromosomes longer than the window (eval_range 300): every trial's
+    window null sums come from its own slot (fsclg_slot_windows per round and device)."""
+    snp = tmp / "tpw.snp"
+    synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=4_000_000, snps_per_chr=4000, n=30, seed=98,
+                                                  sweeps_per_chr=1))
+    opts = ["--coarse-grid-spacing=40000", "--n-permute=45"]
+    run_oracle(snp, tmp / "o.txt", [*opts, "--eval-range=300", f"--throughput-seed={TP_SEED}"], tmp / "o.dump")
+    fscl_amd.reset_stats()
+    try:
+        scan = fscl_amd.run(snp, tmp / "g.txt", permute_mode="throughput", permute_seed=TP_SEED, eval_range=300,
+                            **_kw(opts))
+    finally:
+        fscl_amd.set_permute_mode("parity")
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), "throughput windowed")
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+    assert fscl_amd.get_stats()["window_ms"] > 0
+
+
 def test_throughput_mode_two_ranks(built, tmp, tp_case):
     """Two processes on GPU 0, shared-memory exchange: each rank runs every other trial."""
     snp, opts, want, want_out = tp_case
