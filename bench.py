@@ -372,12 +372,24 @@ def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, 
     gpu = fscl_amd.points(scan)
     orc = OracleScan(snp, threads=threads, asc_depth=cfg.get("asc_depth", 0), asc_min_freq=cfg.get("asc_min_freq", 1))
     orc.scan()
-    ref = orc.clr()
+    ref = orc.points()
     assert len(ref) == len(gpu)
-    d = max((abs(c - g) for (_, _, c), g in zip(ref, gpu["clr"])), default=0.0)
-    m = sum(1 for (ch, p, _), g in zip(ref, gpu) if (ch, p) != (int(g["chr"]), int(g["sweep_pos"])))
-    bl["parity"] = "initial scan, every grid point, against oracle/oracle.c (bit-exact restatement pinned by "\
-                   "the reference's own compiled code, tests/test_oracle.py)"
+    d = rel = 0.0
+    m = ma = mw = bits = 0
+    for r, g in zip(ref, gpu):
+        c, gc = r[2], float(g["clr"])
+        d = max(d, abs(c - gc))
+        if c != 0.0:
+            rel = max(rel, abs(c - gc) / abs(c))
+        m += (r[0], r[1]) != (int(g["chr"]), int(g["sweep_pos"]))
+        ma += r[3].hex() != float(g["lalpha"]).hex()
+        mw += (r[6], r[7], r[8]) != (int(g["nearest_snp"]), int(g["window_start"]), int(g["window_end"]))
+        bits += all(x.hex() == float(g[k]).hex() for x, k in zip(r[2:6], ("clr", "lalpha", "sm_logl", "null_logl")))
+    bl["parity"] = {"what": "initial scan, every grid point, against oracle/oracle.c (bit-exact restatement pinned "
+                            "by the reference's own compiled code, tests/test_oracle.py)",
+                    "points": len(ref), "max_abs_dclr": d, "max_rel_dclr": rel, "position_mismatches": m,
+                    "lalpha_mismatches": ma, "window_mismatches": mw,
+                    "bit_identical_points": bits}
     return bl, d, m
 
 
