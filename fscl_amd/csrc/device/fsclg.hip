@@ -134,6 +134,8 @@ struct Params {
   // split cells (mode 0): `split` workgroups ("members") per cell share every walk's segments and
   // combine their partial sums through a per-cell exchange area in global memory (XAcc, two
   // regions used in turn) and a per-cell arrival counter (zeroed before the launch)
+  int lookahead;               // mode 0: evaluate the next bisection level's predicted midpoint
+                               // beside the current one (FSCLG_LOOKAHEAD=0: one point per search)
   int split;                   // members per cell (1: one workgroup per cell)
   char* xacc;                  // [n_cells][2] XAcc
   unsigned int* xcnt;          // [n_cells] arrivals
@@ -159,7 +161,7 @@ struct Walk {
 };
 
 struct Smem {
-  Pt pt[3];
+  Pt pt[4];                       // cells: start, end, midpoint, the midpoint's predicted child
   Walk w[MAXWALK];
   unsigned long long P[MAXWALK];
   unsigned long long Q[MAXWALK];
@@ -1297,21 +1299,51 @@ __device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
       if (tid == 0) S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps);
       search_maxalpha_pts<LDS, SPLIT>(S, P, 0, 2);  // start and end points share the two phases
     }
+    // the bisection (scan-chromosome.c:103-139), two levels per alpha search: a level goes
+    // left iff (s + m) >= (e + m) (compared exactly as written, :116).  IEEE addition is
+    // monotone, so s >= e makes that true whatever m is, and otherwise it is false unless the
+    // two sums round together (or m is NaN).  The next level's midpoint -- the middle of the
+    // half that s >= e predicts -- is evaluated beside m; when the level's real decision
+    // agrees (nearly always) that level is taken from it at once, otherwise it is dropped and
+    // the next round evaluates the other half's midpoint.  The points evaluated on the path
+    // and every comparison are the reference's; only the number of dependent searches halves.
     int iter = 0;
     for (;;) {
       const int sp = S.pt[0].sweep, ep = S.pt[1].sweep;
       if (ep - sp <= P.bp_resl) break;
       if (++iter > 64) { if (tid == 0) S.pt[0].flags |= PF_NOCONV; break; }
+      const bool pleft = S.pt[0].clr >= S.pt[1].clr;
       if (wave == 0) {
         init_point_wave(S.pt[2], c.chr, (sp + ep) / 2, P, lane);
         if (lane == 0) S.cnt[1] += (unsigned long long)S.pt[2].n_snps;
       }
       __syncthreads();
-      search_maxalpha_pts<LDS, SPLIT>(S, P, 2, 1);
+      // the predicted half ends at the midpoint's own position (init_scan_result may move a
+      // point that sits on a SNP, scan-chromosome.c:67-71)
+      const int m1 = S.pt[2].sweep;
+      const int cs = pleft ? sp : m1, ce = pleft ? m1 : ep;
+      const bool two = P.lookahead && ce - cs > P.bp_resl;
+      if (two) {
+        if (wave == 0) {
+          init_point_wave(S.pt[3], c.chr, (cs + ce) / 2, P, lane);
+          if (lane == 0) S.cnt[1] += (unsigned long long)S.pt[3].n_snps;
+        }
+        __syncthreads();
+      }
+      search_maxalpha_pts<LDS, SPLIT>(S, P, 2, two ? 2 : 1);
+      // every thread takes the same decisions from the same shared values (uniform control)
+      const bool left = (S.pt[0].clr + S.pt[2].clr) >= (S.pt[1].clr + S.pt[2].clr);
+      const bool lvl2 = two && left == pleft;  // the next level, its midpoint already evaluated
+      if (lvl2) ++iter;
+      __syncthreads();
       if (tid == 0) {
-        // scan-chromosome.c:116: compare exactly as written
-        if ((S.pt[0].clr + S.pt[2].clr) >= (S.pt[1].clr + S.pt[2].clr)) S.pt[1] = S.pt[2];
+        if (left) S.pt[1] = S.pt[2];
         else S.pt[0] = S.pt[2];
+        if (lvl2) {
+          if (iter > 64) S.pt[0].flags |= PF_NOCONV;
+          if ((S.pt[0].clr + S.pt[3].clr) >= (S.pt[1].clr + S.pt[3].clr)) S.pt[1] = S.pt[3];
+          else S.pt[0] = S.pt[3];
+        }
       }
       __syncthreads();
     }
@@ -2256,6 +2288,8 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
   P.split = 1; P.xacc = nullptr; P.xcnt = nullptr;
+  static const int lookahead = getenv("FSCLG_LOOKAHEAD") ? atoi(getenv("FSCLG_LOOKAHEAD")) : 1;
+  P.lookahead = lookahead;
   if (getenv("FSCLG_CELL_TRACE")) {
     if (B.ctrace_cap < n) {
       if (B.p_ctrace) hipHostFree(B.p_ctrace);
