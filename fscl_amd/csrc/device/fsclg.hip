@@ -135,7 +135,8 @@ struct Params {
   // combine their partial sums through a per-cell exchange area in global memory (XAcc, two
   // regions used in turn) and a per-cell arrival counter (zeroed before the launch)
   int lookahead;               // mode 0: evaluate the next bisection level's predicted midpoint
-                               // beside the current one (FSCLG_LOOKAHEAD=0: one point per search)
+                               // beside the current one (FSCLG_LOOKAHEAD=0: one point per search;
+                               // 2: mispredict on purpose, the fallback path's test)
   int split;                   // members per cell (1: one workgroup per cell)
   char* xacc;                  // [n_cells][2] XAcc
   unsigned int* xcnt;          // [n_cells] arrivals
@@ -1312,7 +1313,8 @@ __device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
       const int sp = S.pt[0].sweep, ep = S.pt[1].sweep;
       if (ep - sp <= P.bp_resl) break;
       if (++iter > 64) { if (tid == 0) S.pt[0].flags |= PF_NOCONV; break; }
-      const bool pleft = S.pt[0].clr >= S.pt[1].clr;
+      // (FSCLG_LOOKAHEAD=2, tests: predict the other half, so every look-ahead point is dropped)
+      const bool pleft = (S.pt[0].clr >= S.pt[1].clr) != (P.lookahead == 2);
       if (wave == 0) {
         init_point_wave(S.pt[2], c.chr, (sp + ep) / 2, P, lane);
         if (lane == 0) S.cnt[1] += (unsigned long long)S.pt[2].n_snps;

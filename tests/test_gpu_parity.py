@@ -58,6 +58,19 @@ def test_gpu_matches_golden(built, tmp, case):
     assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text()
 
 
+@pytest.mark.parametrize("lookahead", ["0", "2"])
+def test_bisection_lookahead_fallbacks(built, tmp, lookahead):
+    """The two-level bisection with the look-ahead off (one level per alpha
+    search) and with every prediction wrong on purpose (each look-ahead point dropped, the
+    next round evaluates the other half): the golden outputs either way."""
+    for case in ("g1_p25", "g1_asc"):
+        c = manifest()["cases"][case]
+        r = subprocess.run([str(CLI), "-f", str(GOLD / c["input"]), "-o", str(tmp / "o.txt"), *c["options"]],
+                           capture_output=True, text=True, timeout=600, env=dict(os.environ, FSCLG_LOOKAHEAD=lookahead))
+        assert r.returncode == 0, r.stderr
+        assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text(), case
+
+
 @pytest.mark.parametrize("case", ["g1_p25", "g2_grid50k", "g3_scan"])
 def test_cli_matches_golden(built, tmp, case):
     c = manifest()["cases"][case]
