@@ -63,6 +63,9 @@ def parse():
                          "all-reduce callback")
     ap.add_argument("--permute-mode", choices=("parity", "throughput"), default="parity",
                     help="throughput: counter-based random numbers, trials independent (labelled non-parity)")
+    ap.add_argument("--contexts", type=int, default=1,
+                    help="rehearsal only: this process drives N device contexts on its one GPU (the batch and "
+                         "trial split of an N-GPU job, recorded with FSCL_AMD_SIM=record)")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--chromosomes", type=int, default=None,
                     help="chromosomes (default: the config's; development aid)")
@@ -184,7 +187,10 @@ def main() -> int:
                 arr[:] = t.cpu().numpy()
 
             fscl_amd.set_ranks(rank, world, allreduce)
-    fscl_amd.set_device(device)
+    if args.contexts > 1:
+        fscl_amd.set_devices([device] * args.contexts)
+    else:
+        fscl_amd.set_device(device)
 
     cfg = dict(synth.CONFIGS[args.config])
     if args.chromosomes:
