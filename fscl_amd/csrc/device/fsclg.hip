@@ -609,8 +609,9 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
       rv[u] = (!MASK || k < n) ? v.y : 0u;  // zero sentinel row past the segment
     }
     // log distance: when every lane's |d| lies in the LDS copy of the far branch (one
-    // unsigned compare per site: |d| in [2^24, lt_hi << 16)), straight from LDS; otherwise
-    // per lane (logt_lds).  Every lane is active in a trip, so the wave-wide tests below
+    // unsigned compare per site: |d| in [2^24, lt_hi << 16)), straight from LDS; when every
+    // lane's |d| is in the mid branch, one gather each with no branch select; otherwise per
+    // lane (logt_lds).  Every lane is active in a trip, so the wave-wide tests below
     // compare ballots with all ones.
     double x[U];
     uint32_t ad[U];
@@ -620,10 +621,17 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
       ad[u] = absdist(pv[u], usweep);
       far = far && (ad[u] - 0x1000000u < (uint32_t)P.lt_span);
     }
+    bool mid = true;  // every |d| in the mid branch (2^16 <= |d| < 2^24): one global gather each
+#pragma unroll
+    for (int u = 0; u < U; u++) mid = mid && (ad[u] - 0x10000u < 0xFF0000u);
     if (LDS && __builtin_amdgcn_ballot_w64(far) == ~0ull) {
       const double* lt2 = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt);  // pre-offset by -256 entries
 #pragma unroll
       for (int u = 0; u < U; u++) x[u] = lt2[ad[u] >> 16] + la;
+    } else if (__builtin_amdgcn_ballot_w64(mid) == ~0ull) {
+      const char* lt1 = reinterpret_cast<const char*>(P.logt3 + 0x10000);
+#pragma unroll
+      for (int u = 0; u < U; u++) x[u] = *reinterpret_cast<const double*>(lt1 + ((ad[u] >> 8) << 3)) + la;
     } else {
 #pragma unroll
       for (int u = 0; u < U; u++) x[u] = logt_lds<LDS>(ad[u], P) + la;

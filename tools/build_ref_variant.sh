@@ -12,7 +12,7 @@ OUT=$R/fscl_amd/_build_$NAME
 mkdir -p $OUT
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fPIC -std=c++17 -Wno-unused-value -mllvm -amdgpu-sched-strategy=iterative-ilp \
   -Wno-unused-result "$@" -c $T/fscl_amd/csrc/device/fsclg.hip -o $OUT/fsclg.o
-g++ -shared -o $OUT/libfscl_amd.so $R/fscl_amd/_build/{util,input,spectrum,tables,scan}.o $OUT/fsclg.o \
+g++ -shared -o $OUT/libfscl_amd.so $R/fscl_amd/_build/{util,input,spectrum,tables,scan,ranks}.o $OUT/fsclg.o \
   -L/opt/rocm/lib -lamdhip64 -lgomp -lm -lpthread -Wl,-rpath,/opt/rocm/lib
 rm -rf $T
 echo $OUT/libfscl_amd.so
