@@ -367,6 +367,10 @@ def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, 
                     f"{c_scan * 1e3:.2f} ms + {perm_units} trial cells x {c_perm * 1e3:.2f} ms + {trials} serial "
                     f"permutations x {smp['perm_gen_s'] * 1e3:.2f} ms = {job_s:.1f} s",
           "extrapolated": True, "job_s": job_s,
+          "scan_phase_s": gp * c_scan,
+          "perm_sample": {"trial_cells": perm_units, "trial_cell_ms": c_perm * 1e3, "trials": trials,
+                          "serial_permutation_ms": smp["perm_gen_s"] * 1e3,
+                          "perm_phase_s": perm_units * c_perm + trials * smp["perm_gen_s"], "extrapolated": True},
           "threads_1": {"value": units / job1_s, "job_s": job1_s, "sample_cells": one["sample_cells"]},
           "node_linear": {"value": units / node_s, "job_s": node_s, "cores": phys,
                           "note": "one-thread per-cell time / the node's physical cores (perfect scaling, "
