@@ -9,12 +9,21 @@ tables and the null model are set up once before the timed region.
 
 Workload (default, BASELINE.json configs[3], "C4" -- the north star's target
 configuration, which fits one GPU): 22 synthetic chromosomes of 45.45 Mb, 1.0M
-SNPs, n = 200, 10,010 grid cells of 100 kb, 1,000 permutations.  --gpus N (one
-process per GPU, launched by torch.distributed.run) strong-scales the SAME job:
-every rank runs the same host logic (rand stream, permutation, pruning) and
-evaluates a cost-balanced contiguous share of every batch of cells; one
-shared-memory all-gather per batch (the library's own, fscl_amd_set_ranks_shm)
-completes the results on every rank (parity mode: bit-identical to one GPU).
+SNPs, n = 200, 10,010 grid cells of 100 kb, 1,000 permutations.  --gpus N
+strong-scales the SAME job over N GPUs (parity mode: bit-identical to one GPU):
+  * `python bench.py --gpus N` (no launcher): this one process drives GPUs 0..N-1
+    (fscl_amd_set_devices, the CLI's --n-gpus): the host logic -- rand stream,
+    permutation (with its speculative worker threads), pruning -- runs once, and
+    every batch of cells is split into N cost-balanced contiguous shares.  Fewer
+    than N visible GPUs is an error (exit 2).
+  * under torch.distributed.run with N ranks (the driver's SCALE launch): one
+    process per GPU; every rank runs the host logic and evaluates its share of
+    every batch, one shared-memory all-gather per batch (fscl_amd_set_ranks_shm)
+    completes the results on every rank.  --gpus must equal WORLD_SIZE.
+Every timed job's final scan points (every field, floats as hex) are hashed and
+compared with the oracle's digest of the same job (tests/golden/fullsize.json,
+made by tests/golden/make_fullsize.py) where one exists: parity over the whole
+job, the initial scan and all permutation trials with their pruning.
 --config C2 gives BASELINE configs[1].
 
 value = (grid points + sum of permute_n) / wall seconds (max over ranks).
@@ -155,6 +164,35 @@ def issue_roofline(prof: dict) -> dict | None:
     return out
 
 
+def full_job_fixture(snp: Path, opts: list[str]) -> tuple[str | None, dict | None]:
+    """The oracle fixture of exactly this job (same input bytes, same options), if one exists."""
+    import hashlib
+    fx_path = ROOT / "tests" / "golden" / "fullsize.json"
+    if not fx_path.exists():
+        return None, None
+    h = hashlib.sha256(snp.read_bytes()).hexdigest()
+    for name, fx in json.loads(fx_path.read_text()).items():
+        if fx["input_sha256"] == h and sorted(fx["options"]) == sorted(opts):
+            return name, fx
+    return None, None
+
+
+def points_digest(pts) -> tuple[str, list[str]]:
+    """SHA-256 of the canonical point dump (tests/golden/make_fullsize.py: every field of every
+    point in the oracle's dump order, floats as C99 hex) and the canonical rows."""
+    import hashlib
+    fields = ("chr", "sweep_pos", "clr", "lalpha", "sm_logl", "null_logl", "nearest_snp", "window_start",
+              "window_end", "permute_p", "permute_n", "permute_finished")
+    h = hashlib.sha256()
+    rows = []
+    for p in pts:
+        row = "\t".join(x.hex() if isinstance(x, float) else str(x) for x in (p[k].item() for k in fields))
+        rows.append(row)
+        h.update(row.encode())
+        h.update(b"\n")
+    return h.hexdigest(), rows
+
+
 def main() -> int:
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -164,6 +202,17 @@ def main() -> int:
     import torch.distributed as dist
     import fscl_amd
     from fscl_amd import synth
+
+    # --gpus N: N ranks under a launcher, else N devices driven by this process
+    if world > 1 and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} under a launcher with WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    n_local = args.gpus if world == 1 else 1
+    if n_local > 1:
+        vis = fscl_amd.device_count()
+        if vis < n_local:
+            print(f"bench.py: --gpus {n_local} but {vis} GPU(s) visible", file=sys.stderr)
+            return 2
 
     # FSCL_AMD_DEVICE / FSCL_BENCH_BACKEND=gloo: rehearse several ranks on one GPU (tests only)
     device = int(os.environ.get("FSCL_AMD_DEVICE", local))
@@ -189,8 +238,11 @@ def main() -> int:
             fscl_amd.set_ranks(rank, world, allreduce)
     if args.contexts > 1:
         fscl_amd.set_devices([device] * args.contexts)
+    elif n_local > 1:
+        fscl_amd.set_devices(list(range(n_local)))
     else:
         fscl_amd.set_device(device)
+    n_gpus = world * n_local
 
     cfg = dict(synth.CONFIGS[args.config])
     if args.chromosomes:
@@ -214,7 +266,13 @@ def main() -> int:
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        for d in range(n_local):
+            torch.cuda.synchronize(d if n_local > 1 else None)
+
+    job_opts = ([f"--n-permute={n_permute}"] if n_permute > 0 else []) + (
+        [f"--asc-depth={cfg['asc_depth']}", f"--asc-minimum-freq={cfg.get('asc_min_freq', 1)}"]
+        if cfg.get("asc_depth", 0) else [])
+    fx_name, fx = full_job_fixture(snp, job_opts) if rank == 0 and args.permute_mode == "parity" else (None, None)
 
     fscl_amd.set_permute_mode(args.permute_mode)
 
@@ -233,10 +291,13 @@ def main() -> int:
     barrier()
     t0 = time.perf_counter()
     units, gp, n_perm_units = 0, 0, 0
+    timed_pts = []
     for _ in range(args.steps):
         n_gp, n_perm, pts = job()
         units += n_gp + n_perm
         gp, n_perm_units = n_gp, n_perm
+        if fx is not None:
+            timed_pts.append(pts.copy())  # checked after the timed region
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -277,7 +338,7 @@ def main() -> int:
         "metric": METRIC,
         "value": units / elapsed,
         "unit": UNIT,
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -291,9 +352,17 @@ def main() -> int:
                                f"{n_permute} permutations, "
                                + ("parity mode" if args.permute_mode == "parity" else
                                   "THROUGHPUT MODE (counter-based random numbers: non-parity, not the metric's mode)")
-                               + f", one job split over {world} GPU(s)",
+                               + f", one job split over {n_gpus} GPU(s)",
                    "grid_points": gp, "n_permute": n_permute, "snps": cfg["snps_per_chr"] * cfg["n_chr"],
-                   "units_per_step": units / args.steps, "exchange": args.exchange if world > 1 else None},
+                   "units_per_step": units / args.steps,
+                   "multi_gpu": (f"{world} processes, one GPU each, shared-memory all-gather per batch "
+                                 f"(exchange: {args.exchange})" if world > 1 else
+                                 f"one process driving {n_local} GPUs" if n_local > 1 else None),
+                   # work shared between cells, identical results: a units/s comparison
+                   # with the reference, which recomputes them, should read these
+                   "dup_cells_per_step": st["n_dup_cells"] / args.steps,
+                   "endpoint_evals_saved_per_step": st["n_ep_saved"] / args.steps,
+                   "negj_per_step": st["negj"] / args.steps},
         "roofline": roof,
         "cpu_baseline": None,
         "max_abs_dclr": None,
@@ -306,6 +375,32 @@ def main() -> int:
                                      "spec_hits", "spec_cands", "spec_wait_s", "spec_done", "spec_gen_s")},
     }
 
+    # ---- parity of every timed job, whole job: initial scan + all permutation trials, their
+    # hits, prune draws and saved null CLRs, against the oracle's digest of the same job
+    if fx is not None:
+        digs = [points_digest(p) for p in timed_pts]
+        ok = [d == fx["dump_sha256"] for d, _ in digs]
+        bad_rows = 0
+        if not all(ok):  # locate: the fixture's sampled rows
+            k = fx["sample_every"]
+            rows = next(r for (d, r), o in zip(digs, ok) if not o)
+            bad_rows = sum(rows[i * k] != want for i, want in enumerate(fx["sample"]))
+        out["parity"] = {"scope": "full job", "fixture": f"tests/golden/fullsize.json[{fx_name}]",
+                         "what": "SHA-256 of every field of every final scan point (CLR, lalpha, sm_logl, null_logl "
+                                 "as hex; positions, windows; permute_p, permute_n, permute_finished) of each timed "
+                                 "job against the oracle's run of the same job (oracle/oracle.c, pinned by the "
+                                 "reference's own compiled code)",
+                         "jobs_checked": len(ok), "jobs_identical": sum(ok), "points": fx["n_points"],
+                         "sum_permute_n": fx["sum_permute_n"], "sampled_rows_differing": bad_rows,
+                         "negj_per_job": st["negj"] / args.steps}
+        out["max_abs_dclr"] = 0.0 if all(ok) else None
+        if not all(ok):
+            print(f"bench.py: PARITY FAILURE: {len(ok) - sum(ok)} of {len(ok)} timed jobs differ from {fx_name}",
+                  file=sys.stderr)
+    elif rank == 0:
+        out["parity"] = {"scope": "initial scan" if world == 1 and n_local == 1 and not args.no_cpu_baseline else
+                         "none in this run", "note": "no oracle fixture of this exact job (tests/golden/fullsize.json)"}
+
     # ---- CPU baseline (rank 0, one GPU): the reference's own compiled hot path
     # (oracle/_ref/ref_harness: sm-search.c / sm-spline.c / background / asc-bias / input
     # compiled from its sources, under oracle.c's restated scan loop -- scan-chromosome.c
@@ -315,17 +410,21 @@ def main() -> int:
     # times and the job's own counts.  Then the GPU's initial scan is checked against the
     # reference code's on a spread sample of cells... and against the oracle on all cells.
     # Test infrastructure: timed and compared here, never called by the product.
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         info = cpu_info()
-        out["cpu_baseline"], out["max_abs_dclr"], out["position_mismatches"] = cpu_baseline(
+        out["cpu_baseline"], scan_dclr, out["position_mismatches"] = cpu_baseline(
             args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, n_perm_units, st["trials"] // max(1, args.steps),
             units / args.steps, elapsed / args.steps)
+        if out["max_abs_dclr"] is None or fx is None:
+            out["max_abs_dclr"] = scan_dclr
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     fscl_amd.shutdown()
+    if out.get("parity", {}).get("scope") == "full job" and out["parity"]["jobs_identical"] != out["parity"]["jobs_checked"]:
+        return 1
     return 0
 
 

@@ -71,7 +71,7 @@ def _build_native(force: bool, trace: bool, defines: tuple[str, ...] = ()) -> Pa
         s = CSRC / "host" / src
         o = OUT / (s.stem + ".o")
         if force or _stale(o, [s, *hdrs]):
-            _run(["gcc", *CFLAGS, "-c", s, "-o", o])
+            _run(["gcc", *CFLAGS, *defines, "-c", s, "-o", o])
         objs.append(o)
     hip_src = CSRC / "device" / "fsclg.hip"
     hip_obj = OUT / "fsclg.o"
@@ -103,6 +103,8 @@ def main(argv: list[str]) -> int:
     build_native(force=force)
     if "--trace" in argv:
         build_native(force=force, trace=True)
+    if "--rehearsal" in argv:  # the scaling-rehearsal test build (tools/scale_sim.sh)
+        build_native(force=force, variant="rehearsal", defines=("-DFSCL_AMD_REHEARSAL",))
     if "--no-oracle" not in argv:
         build_oracle()
     return 0

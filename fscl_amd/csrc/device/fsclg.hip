@@ -1555,6 +1555,7 @@ struct Batch {
   bool pending = false;
   int split_max = 1;                // fsclg_set_batch_split
   int split = 1;                    // members per cell of the current launch
+  int eval_range = 0, bp_resl = 0;  // of the submitted launch (a split launch re-run unsplit)
   char* d_xacc = nullptr;           // split cells' accumulators and arrival counters
   unsigned int* d_xcnt = nullptr;
   size_t xacc_cap = 0;
@@ -1609,6 +1610,7 @@ struct fsclg_ctx {
   unsigned long long* d_stats = nullptr;
   std::unordered_map<unsigned long long, uint32_t> cell_cost;  // (chr, start, end) -> cost of its last run
   unsigned long long n_dup_cells = 0, n_ep_saved = 0;
+  unsigned long long n_split_retry = 0;
   double kernel_ms = 0.0;
   unsigned long long launches = 0;
   std::vector<std::pair<double, double>> busy;  // [start, end) ms of each batch's kernels since ev_ref
@@ -2384,6 +2386,7 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
   B.n_cells = n_cells; B.nu = 0; B.nlaunch = 0; B.slot = slot; B.ivhist = nullptr; B.traced = false;
+  B.eval_range = eval_range; B.bp_resl = bp_resl;
   if (n_cells == 0) {
     B.pending = true;
     c->slot[slot].users++;
@@ -2626,6 +2629,26 @@ int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
   for (int k = 0; k < nu; k++)
     if (B.p_cells[k].chr >= 0) c->cell_cost[cell_key(B.p_cells[k])] = B.p_out[k].cost;
   for (int i = 0; i < B.n_cells; i++) out[i] = B.p_out[B.upos[B.uidx[i]]];
+  // a split cell whose members were not all resident at once (a member waited > ~1 s: a busy
+  // or shared device) has no result: the launch is run again with one workgroup per cell,
+  // which needs no co-residency and gives the same results
+  bool retry = false;
+  for (int i = 0; i < B.n_cells && !retry; i++) retry = (out[i].flags & PF_SPLIT_TIMEOUT) && B.split > 1;
+  {  // FSCLG_FORCE_SPLIT_RETRY=n (tests): treat the first n split launches as timed out
+    static int forced = getenv("FSCLG_FORCE_SPLIT_RETRY") ? atoi(getenv("FSCLG_FORCE_SPLIT_RETRY")) : 0;
+    if (!retry && B.split > 1 && forced > 0) { forced--; retry = true; }
+  }
+  if (retry) {
+    std::vector<fsclg_cell_t> cells(B.n_cells);
+    for (int i = 0; i < B.n_cells; i++) cells[i] = B.ucells[B.uidx[i]];
+    const int saved = B.split_max;
+    c->n_split_retry++;
+    B.split_max = 1;
+    int r = fsclg_search_submit(c, batch, B.slot, cells.data(), B.n_cells, B.eval_range, B.bp_resl);
+    B.split_max = saved;
+    if (r) return r;
+    return fsclg_search_wait(c, batch, out);
+  }
   for (int i = 0; i < B.n_cells; i++)
     if (out[i].flags)
       return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL,
@@ -2729,6 +2752,7 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
   for (int k = 0; k < NSLOT; k++) window_time(c, c->slot[k]);
   st->kernel_ms = c->kernel_ms; st->n_launches = c->launches; st->window_ms = c->window_ms;
   st->n_dup_cells = c->n_dup_cells; st->n_ep_saved = c->n_ep_saved;
+  st->n_split_retry = c->n_split_retry;
   {  // union of the batches' kernel intervals
     std::vector<std::pair<double, double>> iv(c->busy);
     std::sort(iv.begin(), iv.end());
@@ -2750,7 +2774,7 @@ int fsclg_reset_stats(fsclg_ctx* c) {
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
   for (int k = 0; k < NSLOT; k++) window_time(c, c->slot[k]);  // pending times belong before the reset
-  c->kernel_ms = 0.0; c->launches = 0; c->window_ms = 0.0; c->n_dup_cells = 0; c->n_ep_saved = 0;
+  c->kernel_ms = 0.0; c->launches = 0; c->window_ms = 0.0; c->n_dup_cells = 0; c->n_ep_saved = 0; c->n_split_retry = 0;
   c->busy.clear();
   return FSCLG_OK;
 }

@@ -57,6 +57,7 @@ typedef struct fh_shm fh_shm_t;
 fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap);
 void fh_shm_close(fh_shm_t *m);
 int fh_shm_allgather(fh_shm_t *m, void *buf, size_t item, int n, int lo, int hi);
+int fh_shm_allgather_flags(fh_shm_t *m, void *buf, size_t item, int n, int lo, int hi, unsigned *flags);
 int fh_shm_barrier(fh_shm_t *m);
 
 /* ms reader */

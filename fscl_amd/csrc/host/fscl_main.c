@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "fscl_host.h"
 
@@ -191,11 +192,13 @@ int main(int argc, char **argv) {
       /* one process per GPU (e.g. under torch.distributed.run): GPU $LOCAL_RANK (or
          $FSCL_AMD_DEVICE), results exchanged through a shared-memory segment named by
          $FSCL_AMD_SHM_NAME, else the launcher's run id or port; rank 0 writes the output */
-      const char *id = getenv("FSCL_AMD_SHM_NAME");
-      char name[160];
-      if (!id) id = getenv("TORCHELASTIC_RUN_ID");
-      if (!id) id = getenv("MASTER_PORT");
-      snprintf(name, sizeof name, "/fscl_amd_%s", id ? id : "job");
+      const char *id = getenv("FSCL_AMD_SHM_NAME"), *run = getenv("TORCHELASTIC_RUN_ID"), *port = getenv("MASTER_PORT");
+      char name[200];
+      if (id) snprintf(name, sizeof name, "/fscl_amd_%s", id);
+      else /* the launcher's run id (plain torchrun sets "none"), its port, and the parent's pid: the
+              ranks of one launch share their parent (the launcher), two jobs on a node do not */
+        snprintf(name, sizeof name, "/fscl_amd_%s_%s_%ld", run && strcmp(run, "none") ? run : "job", port ? port : "0",
+                 (long)getppid());
       if (n_gpus > 1) logmsg(MSG_WARN, "Warning: --n-gpus is ignored with one process per GPU (WORLD_SIZE=%s).\n", ws);
       if (fscl_amd_set_ranks_shm(atoi(rk), atoi(ws), name) != 0)
         logmsg(MSG_FATAL, "fscl: rank %s of %s could not meet the other ranks (%s)", rk, ws, name);

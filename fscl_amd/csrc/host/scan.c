@@ -203,28 +203,56 @@ static void dev_check(int r, const char *what) {
   if (r != FSCLG_OK) logmsg(MSG_FATAL, "fscl_amd: %s failed: %s (code %d)", what, fsclg_last_error(), r);
 }
 
-/* FSCL_AMD_SIM=record:<file> (one process, all shares) writes every batch's results;
-   FSCL_AMD_SIM=replay:<file>:<world>[:<rank>] runs as one rank of a `world`-process job:
-   it evaluates only its own share and takes the others from the recording (checking its
-   own bit for bit).  Development aid: the time of a W-rank job's rank on one GPU. */
+/* Scaling rehearsal (test build only: -DFSCL_AMD_REHEARSAL, fscl_amd/_build_rehearsal,
+   tools/scale_sim.sh).  FSCL_AMD_SIM=record:<file> (one process, all shares) writes every
+   batch's results; FSCL_AMD_SIM=replay:<file>:<world>[:<rank>] runs as one rank of a
+   `world`-process job: it evaluates only its own share and takes the others from the recording
+   (checking its own bit for bit) -- the time of a W-rank job's rank on one GPU.  The product
+   library has no such hook: it refuses the variable. */
 static void sim_init(void) {
   static int done = 0;
   const char *e = getenv("FSCL_AMD_SIM");
-  char path[1024];
-  int w = 1, r = 0;
   if (done) return;
   done = 1;
   if (!e) return;
-  if (sscanf(e, "record:%1023[^:]", path) == 1 && !strncmp(e, "record:", 7)) {
-    D.sim = fopen(path, "wb");
-    D.sim_replay = 0;
-  } else if (!strncmp(e, "replay:", 7) && sscanf(e + 7, "%1023[^:]:%d:%d", path, &w, &r) >= 2) {
-    D.sim = fopen(path, "rb");
-    D.sim_replay = 1;
-    D.world = w; D.rank = r; D.xfn = NULL; D.shm = NULL;
+#ifdef FSCL_AMD_REHEARSAL
+  {
+    char path[1024];
+    int w = 1, r = 0;
+    if (sscanf(e, "record:%1023[^:]", path) == 1 && !strncmp(e, "record:", 7)) {
+      D.sim = fopen(path, "wb");
+      D.sim_replay = 0;
+    } else if (!strncmp(e, "replay:", 7) && sscanf(e + 7, "%1023[^:]:%d:%d", path, &w, &r) >= 2) {
+      D.sim = fopen(path, "rb");
+      D.sim_replay = 1;
+      D.world = w; D.rank = r; D.xfn = NULL; D.shm = NULL;
+    }
+    if (!D.sim) logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM=%s: cannot open the file", e);
   }
-  if (!D.sim) logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM=%s: cannot open the file", e);
+#else
+  logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM is a scaling-rehearsal hook of the test build (fscl_amd/_build_rehearsal)");
+#endif
 }
+
+#ifdef FSCL_AMD_REHEARSAL
+/* the rehearsal's exchange: record the batch, or replay the other ranks' shares */
+static void sim_exchange(fsclg_point_t *out, int n, int lo, int hi) {
+  if (!D.sim_replay) {
+    if (fwrite(&n, sizeof n, 1, D.sim) != 1 || fwrite(out, sizeof(fsclg_point_t), (size_t)n, D.sim) != (size_t)n)
+      logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM record write failed");
+  } else {
+    fsclg_point_t *rec = fh_malloc(sizeof(fsclg_point_t) * (n ? n : 1), "sim");
+    int m = -1, i;
+    if (fread(&m, sizeof m, 1, D.sim) != 1 || m != n || fread(rec, sizeof(fsclg_point_t), (size_t)n, D.sim) != (size_t)n)
+      logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM replay: batch of %d cells, recording has %d", n, m);
+    for (i = lo; i < hi; i++)
+      if (memcmp(&rec[i].lalpha, &out[i].lalpha, 4 * sizeof(double)) != 0)
+        logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM replay: cell %d of a batch differs from the recording", i);
+    memcpy(out, rec, sizeof(fsclg_point_t) * (size_t)n);
+    free(rec);
+  }
+}
+#endif
 
 static void dev_open(void) {
   int l, n;
@@ -479,23 +507,9 @@ static void dev_shares(const double *cost, int n, int *lo, int *hi) {
 
 /* complete a batch's results on every rank: this process holds [lo, hi) of out[n] */
 static void exchange_points(fsclg_point_t *out, int n, int lo, int hi) {
-  if (D.sim) {
-    if (!D.sim_replay) {
-      if (fwrite(&n, sizeof n, 1, D.sim) != 1 || fwrite(out, sizeof(fsclg_point_t), (size_t)n, D.sim) != (size_t)n)
-        logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM record write failed");
-    } else {
-      fsclg_point_t *rec = fh_malloc(sizeof(fsclg_point_t) * (n ? n : 1), "sim");
-      int m = -1, i;
-      if (fread(&m, sizeof m, 1, D.sim) != 1 || m != n || fread(rec, sizeof(fsclg_point_t), (size_t)n, D.sim) != (size_t)n)
-        logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM replay: batch of %d cells, recording has %d", n, m);
-      for (i = lo; i < hi; i++)
-        if (memcmp(&rec[i].lalpha, &out[i].lalpha, 4 * sizeof(double)) != 0)
-          logmsg(MSG_FATAL, "fscl_amd: FSCL_AMD_SIM replay: cell %d of a batch differs from the recording", i);
-      memcpy(out, rec, sizeof(fsclg_point_t) * (size_t)n);
-      free(rec);
-    }
-    return;
-  }
+#ifdef FSCL_AMD_REHEARSAL
+  if (D.sim) { sim_exchange(out, n, lo, hi); return; }
+#endif
   if (D.world <= 1 || n == 0) return;
   if (D.shm) {
     if (fh_shm_allgather(D.shm, out, sizeof(fsclg_point_t), n, lo, hi) != 0)
@@ -738,6 +752,25 @@ static void on_sigint(int sig) { /* scan-chromosome.c:557-569 */
 }
 
 static void output_clr_null_distribution(const char *fname, scan_t *s);
+
+/* whether to dump now: with several ranks the dump is collective -- every rank drains its
+   bulk batches and dumps at the same trial, so they keep making the same exchanges.  Each
+   rank's flag goes into one exchange made at the same point of every trial (round); all ranks
+   act on the OR.  A signal that arrives after this trial's exchange counts at the next. */
+static int sigint_agreed(void) {
+  unsigned f = g_sigint ? 1u : 0u;
+  if (D.world <= 1 || D.sim) return (int)f;
+  if (D.shm) {
+    char dummy = 0;
+    if (fh_shm_allgather_flags(D.shm, &dummy, 1, 0, 0, 0, &f) != 0) logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
+    return f != 0;
+  }
+  {
+    long long v = f;
+    if (D.xfn(&v, 1, D.xctx) != 0) logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
+    return v != 0;
+  }
+}
 
 /* scan-chromosome.c:553-560, taken between trials: the current table and null distributions
    (one writer: rank 0); every rank restarts its 10-second window, so a second interrupt
@@ -1289,7 +1322,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       fprintf(tt, "%d %d %d %d %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n", trial, n_act, A.n, B->n,
               (tr[1] - tr[0]) * 1e6, (tr[2] - tr[1]) * 1e6, (tr[3] - tr[2]) * 1e6, (tr[4] - tr[3]) * 1e6,
               (tr[5] - tr[4]) * 1e6, (fh_now() - tr[5]) * 1e6, tr[6], tr[7]);
-    if (g_sigint) {
+    if (sigint_agreed()) {
       /* the dump shows every trial up to this one: the bulk results still in flight first
          (no draws among them) */
       for (;;) {
@@ -1586,7 +1619,7 @@ static void permute_throughput(scan_t *s, int n_perm, double permute_nbp, int ev
       }
       D.st.prune_s += fh_now() - tw;
       r_done++;
-      if (g_sigint) sigint_dump(s, n_perm); /* every trial applied so far */
+      if (sigint_agreed()) sigint_dump(s, n_perm); /* every trial applied so far */
     }
   }
   D.st.negj += TB.negj;
@@ -1682,7 +1715,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
         fprintf(stderr, "%d\t%d\t%g\t%1.3e\n", q->chr, cells[i].start_pos, clr, exp(out[i].lalpha));
     }
     D.st.prune_s += fh_now() - tp;
-    if (g_sigint) sigint_dump(s, n_perm);
+    if (sigint_agreed()) sigint_dump(s, n_perm);
   }
   free(act); free(cells); free(out); free(nul);
 done:
@@ -1758,7 +1791,7 @@ static void dropin_tables(const sm_ptable_t *sm, int n_depths, const snp_t *snps
   DI.n = 0;  /* the tables were replaced: the sites go up again */
 }
 
-void search_maxalpha(scan_pt_t *pt, snp_t *snps, sm_ptable_t *sm) {
+static void search_maxalpha_locked(scan_pt_t *pt, snp_t *snps, sm_ptable_t *sm) {
   const int ws = pt->window_start, we = pt->window_end, n = we - ws + 1;
   int i, maxd = 0, need_tables, reuse;
   fsclg_point_t p;
@@ -1809,6 +1842,17 @@ void search_maxalpha(scan_pt_t *pt, snp_t *snps, sm_ptable_t *sm) {
   p.window_start = ws - DI.lo; p.window_end = we - DI.lo; p.null_logl = pt->null_logl;
   dev_check(fsclg_search_points(DI.ctx, &p, 1), "search_maxalpha");
   pt->lalpha = p.lalpha; pt->sm_logl = p.sm_logl; pt->clr = p.clr;
+}
+
+/* the reference calls search_maxalpha from its --n-threads workers (scan-chromosome.c:258,
+   514, 531): the drop-in's state (DI: context, tables, the resident window) is shared, so
+   calls are serialised; each is one short device launch */
+static pthread_mutex_t g_dropin_mu = PTHREAD_MUTEX_INITIALIZER;
+
+void search_maxalpha(scan_pt_t *pt, snp_t *snps, sm_ptable_t *sm) {
+  pthread_mutex_lock(&g_dropin_mu);
+  search_maxalpha_locked(pt, snps, sm);
+  pthread_mutex_unlock(&g_dropin_mu);
 }
 
 /* ---------------------------------------------------------------- output */
@@ -1896,7 +1940,7 @@ void fscl_amd_get_stats(fscl_amd_stats_t *st) {
   *st = D.st;
   st->kernel_ms = 0; st->n_terms = st->n_null = st->n_walks = st->n_maxalpha = 0;
   st->n_unsafe = st->n_slow = st->n_ties = st->n_launches = 0;
-  st->window_ms = 0; st->n_dup_cells = st->n_ep_saved = 0; st->busy_ms = 0;
+  st->window_ms = 0; st->n_dup_cells = st->n_ep_saved = 0; st->busy_ms = 0; st->n_split_retry = 0;
   for (l = 0; l < D.n_dev; l++) {
     fsclg_stats_t g;
     if (fsclg_get_stats(D.ctx[l], &g) != FSCLG_OK) continue;
@@ -1906,6 +1950,7 @@ void fscl_amd_get_stats(fscl_amd_stats_t *st) {
     st->window_ms += g.window_ms;
     st->n_dup_cells += g.n_dup_cells; st->n_ep_saved += g.n_ep_saved;
     st->busy_ms += g.busy_ms;
+    st->n_split_retry += g.n_split_retry;
     if (l == 0) {
       st->cache_iv0 = g.cache_iv0; st->cache_n_iv = g.cache_n_iv; st->cache_n_rows = g.cache_n_rows;
       st->cache_cover = g.cache_cover;

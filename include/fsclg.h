@@ -75,6 +75,8 @@ typedef struct {
   unsigned long long n_ep_saved;   /* endpoint evaluations saved by sharing between neighbouring cells */
   double busy_ms;                  /* union of the search batches' kernel intervals (overlapping batches
                                       counted once): the GPU time the search kernels occupied */
+  unsigned long long n_split_retry; /* split launches whose members were not resident together (a
+                                       member waited > ~1 s), re-run with one workgroup per cell */
 } fsclg_stats_t;
 
 /* trials in flight: row slots (one permuted row array + null sums each) and launch batches

@@ -16,6 +16,8 @@ Cases (SURVEY §8(d) / BASELINE.json):
   C4_full_p2  22 x 45k SNPs (1.0M), n=200, --n-permute=2         (configs[3] genome)
   C5_full     22 x 227k SNPs (5.0M), n=400, initial scan          (configs[4] genome)
   C5_chr_p200 one C5 chromosome, --n-permute=200 (early prune)    (configs[4] regime)
+  C4_bench_p1000  bench.py's default job exactly (seed 1), --n-permute=1000 (configs[3], the metric's job)
+  C5_full_p25 the C5 genome (seed 55), --n-permute=25 (windowed null sums per trial, first prunes)
 """
 from __future__ import annotations
 
@@ -43,6 +45,14 @@ CASES = {
                     opts=[]),
     "C5_chr_p200": dict(gen=dict(n_chr=1, chr_len=227_272_727, snps_per_chr=227_273, n=400, seed=57,
                                  sweeps_per_chr=2), opts=["--n-permute=200"]),
+    # bench.py's own default job, exactly (seed 1, synth.CONFIGS["C4"], 1000 permutations): bench.py
+    # checks every timed job's final points against this digest (parity scope "full job")
+    "C4_bench_p1000": dict(gen=dict(n_chr=22, chr_len=45_454_545, snps_per_chr=45_455, n=200, folded=0.0, seed=1,
+                                    sweeps_per_chr=2), opts=["--n-permute=1000"]),
+    # the whole C5 genome with permutations: per-trial windowed null sums on every chromosome and
+    # the first prune draws (permute_p reaches 20 only after 20 trials)
+    "C5_full_p25": dict(gen=dict(n_chr=22, chr_len=227_272_727, snps_per_chr=227_273, n=400, folded=0.0, seed=55,
+                                 sweeps_per_chr=2), opts=["--n-permute=25"]),
 }
 
 

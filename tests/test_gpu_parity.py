@@ -534,6 +534,134 @@ def test_sigint_dumps_table_and_null_distribution(built, tmp):
     assert (tmp / "g.txt-nulldist").read_text() == (tmp / "o.txt-nulldist").read_text()
 
 
+def test_sigint_with_two_ranks_dumps_collectively(built, tmp):
+    """One process per GPU (both ranks on GPU 0 here), SIGINT delivered to rank 1 alone -- the
+    rank that writes nothing.  The dump decision is collective (each rank's flag rides on one
+    exchange per trial, every rank acts on the OR: ADVICE r02), so both ranks drain their bulk
+    batches at the same trial, keep exchanging the same batches, and rank 0 writes the table and
+    <output>-nulldist; they equal the oracle's for that many permutations.  A second interrupt
+    to both ranks within the window ends both (exit 255)."""
+    import re
+    import signal
+    import threading
+    import time
+    snp = tmp / "sig2.snp"
+    synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=6_000_000, snps_per_chr=6000, n=30, seed=97,
+                                                  sweeps_per_chr=2))
+    out = tmp / "g.txt"
+    env = dict(os.environ, FSCL_AMD_SIGINT_WINDOW_MS="300", WORLD_SIZE="2", FSCL_AMD_DEVICE="0",
+               FSCL_AMD_SHM_NAME=f"sig2_{os.getpid()}", FSCL_AMD_RANK_TIMEOUT="60", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([str(CLI), "-f", str(snp), "-o", str(out), "--coarse-grid-spacing=60000",
+                               "--n-permute=1000000"], stderr=subprocess.PIPE, env=dict(env, RANK=str(r)))
+             for r in range(2)]
+    seen = [-1, -1]
+
+    def reader(r):
+        buf = b""
+        while True:
+            ch = procs[r].stderr.read(256)
+            if not ch:
+                return
+            buf = (buf + ch)[-4096:]
+            for m in re.finditer(rb"permutations\.\.\.\s+(\d+) \(", buf):
+                seen[r] = max(seen[r], int(m.group(1)))
+
+    ths = [threading.Thread(target=reader, args=(r,), daemon=True) for r in range(2)]
+    for th in ths:
+        th.start()
+    try:
+        t0 = time.time()
+        while min(seen) < 0:
+            assert all(p.poll() is None for p in procs), "a rank ended before the permutations"
+            assert time.time() - t0 < 300, "no permutation progress"
+            time.sleep(0.005)
+        t1 = time.time()
+        while min(seen) < 60 or time.time() - t1 < 0.6:
+            assert all(p.poll() is None for p in procs), "a rank ended before the interrupt"
+            time.sleep(0.005)
+        at = seen[1]
+        procs[1].send_signal(signal.SIGINT)  # the non-writing rank only
+        t2 = time.time()
+        nd = tmp / "g.txt-nulldist"
+        n_pts = None
+        while True:
+            assert all(p.poll() is None for p in procs), f"a rank ended after the interrupt (trial {at})"
+            assert time.time() - t2 < 60, "no dump from rank 0"
+            if nd.exists() and out.exists():
+                if n_pts is None:
+                    n_pts = len(out.read_text().splitlines()) or None
+                txt = nd.read_text()
+                if n_pts and txt.endswith("\n") and txt.count("\n") == n_pts + 1:
+                    break
+            time.sleep(0.0005)
+        for p in procs:
+            p.send_signal(signal.SIGINT)
+        rcs = [p.wait(timeout=60) for p in procs]
+        assert rcs == [255, 255], rcs
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for th in ths:
+        th.join(timeout=10)
+    rows = [line.split("\t") for line in out.read_text().splitlines()]
+    n_trials = max(int(r[5]) for r in rows)
+    assert n_trials > 60
+    run_oracle(snp, tmp / "o.txt", ["--coarse-grid-spacing=60000", f"--n-permute={n_trials - 1}", "--nulldist"])
+    assert out.read_text() == (tmp / "o.txt").read_text()
+    assert (tmp / "g.txt-nulldist").read_text() == (tmp / "o.txt-nulldist").read_text()
+
+
+def test_split_timeout_reruns_unsplit(built, tmp, monkeypatch):
+    """A split launch whose members were not co-resident (PF_SPLIT_TIMEOUT) is re-run with one
+    workgroup per cell instead of failing the job; forced here for the first 3
+    split launches (FSCLG_FORCE_SPLIT_RETRY): same results as the oracle, retries counted."""
+    c = manifest()["cases"]["g1_p25"]
+    monkeypatch.setenv("FSCLG_FORCE_SPLIT_RETRY", "3")
+    fscl_amd.reset_stats()
+    fscl_amd.run(GOLD / c["input"], tmp / "g.txt", **_kw(c["options"]))
+    assert fscl_amd.get_stats()["n_split_retry"] == 3
+    assert (tmp / "g.txt").read_text() == (GOLD / "g1_p25.out").read_text()
+
+
+def test_dropin_search_maxalpha_from_threads(built):
+    """The reference calls search_maxalpha from its --n-threads workers (scan-chromosome.c:258,
+    514, 531): concurrent calls into the drop-in (serialised inside) each get their
+    own point's golden result, with the golden case's points and a second genome's interleaved
+    (the drop-in's resident window and tables change between calls)."""
+    import ctypes as C
+    from concurrent.futures import ThreadPoolExecutor
+    L = fscl_amd.get_lib()
+    jobs = []
+    for case in ("g2_p30", "g1_p25"):
+        c = manifest()["cases"][case]
+        scan = fscl_amd.load_snp_input(GOLD / c["input"])
+        fsp = fscl_amd.background_fsp(scan)
+        tab = fscl_amd.compute_sweep_model_tables(scan, fsp)
+        fscl_amd.compute_snp_null_model(scan, fsp)
+        for row in read_dump(GOLD / f"{case}.dump")[:40]:
+            jobs.append((scan, tab, row))
+    keep = [j[:2] for j in jobs]  # the scans and tables stay alive while the threads run
+
+    def call(job):
+        scan, tab, row = job
+        pt = fscl_amd.ScanPtT()
+        pt.chr, pt.sweep_pos = row[0], row[1]
+        pt.null_logl = row[5]
+        pt.nearest_snp, pt.window_start, pt.window_end = row[6], row[7], row[8]
+        pt.n_snps = row[8] - row[7] + 1
+        pt.sm_logl, pt.lalpha = -1.7976931348623157e308, 4.0
+        L.search_maxalpha(C.byref(pt), scan.contents.snps, tab)
+        return (pt.lalpha.hex(), pt.sm_logl.hex(), pt.clr.hex()), (row[3].hex(), row[4].hex(), row[2].hex())
+
+    order = [jobs[k // 2] if k % 2 == 0 else jobs[len(jobs) // 2 + k // 2] for k in range(len(jobs))]
+    with ThreadPoolExecutor(8) as ex:
+        for got, want in ex.map(call, order * 2):
+            assert got == want
+    assert keep
+
+
 # ---------------------------------------------------------------- throughput mode
 TP_SEED = 0x5EED1234
 

@@ -122,3 +122,49 @@ def test_device_shares_are_contiguous_and_cover(built):
             tot = cost.sum()
             for lo, hi in spans:  # no share far above its part of the cost
                 assert cost[lo:hi].sum() <= tot / T + (cost.max() if n else 0) + 1e-9
+
+
+SHM_CHECK_WORKER = r"""
+import ctypes as C, os, sys
+import numpy as np
+sys.path.insert(0, os.environ["REPO"])
+import fscl_amd
+L = fscl_amd.get_lib()
+L.fh_shm_open.restype = C.c_void_p
+L.fh_shm_open.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_size_t]
+L.fh_shm_allgather_flags.restype = C.c_int
+L.fh_shm_allgather_flags.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                     C.POINTER(C.c_uint)]
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+m = L.fh_shm_open(rank, world, os.environ["SHM_NAME"].encode(), 1 << 20)
+assert m, "attach"
+buf = np.zeros(16, dtype=np.int64)
+for it in range(50):  # the OR of every rank's flag word, the same on every rank
+    f = C.c_uint((1 << rank) if it % (rank + 2) == 0 else 0)
+    assert L.fh_shm_allgather_flags(m, buf.ctypes.data, 8, 16, 0, 0, C.byref(f)) == 0
+    want = sum(1 << r for r in range(world) if it % (r + 2) == 0)
+    assert f.value == want, (rank, it, f.value, want)
+# control flow diverges: rank 1 exchanges a batch of a different size -> every rank fails
+n = 16 if rank != 1 else 12
+f = C.c_uint(0)
+r = L.fh_shm_allgather_flags(m, buf.ctypes.data, 8, n, 0, 0, C.byref(f))
+assert r != 0, "size mismatch not detected"
+print("ok", rank)
+"""
+
+
+def test_shared_memory_exchange_flags_and_divergence(built, tmp_path):
+    """ranks.c: every exchange carries a flag word (the OR over ranks: the collective SIGINT
+    dump decision) and a (sequence, size) check -- ranks that exchange different batches
+    fail instead of mixing results."""
+    script = tmp_path / "c.py"
+    script.write_text(SHM_CHECK_WORKER)
+    env = dict(os.environ, WORLD_SIZE="3", REPO=str(ROOT), SHM_NAME=f"/fscl_amd_testc_{os.getpid()}",
+               FSCL_AMD_RANK_TIMEOUT="60")
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(3)]
+    for p in procs:
+        out, err = p.communicate(timeout=300)
+        assert p.returncode == 0, err
+        assert "ok" in out.split(), out
+        assert "rank exchange mismatch" in err

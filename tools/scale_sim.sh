@@ -5,6 +5,8 @@
 #    the other shares from the recording (rank 0's own share is checked bit for bit) -- and
 #    time it: the job time of one rank of a W-GPU run, minus the real exchange latency.
 set -e
+# the rehearsal hook lives only in the test build: python -m fscl_amd.build --rehearsal (in the container)
+export FSCL_AMD_LIBDIR=${GRAFT_REPO_ROOT:-$PWD}/fscl_amd/_build_rehearsal
 CFG=$1; TAG=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$R/gpurun_out/sim_$TAG

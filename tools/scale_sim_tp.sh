@@ -5,6 +5,7 @@
 # 2. replay as rank 0 of W: evaluate only rank 0's share (its trials, in throughput mode), take the
 #    rest from the recording (rank 0's own results checked bit for bit), and time it.
 set -e
+export FSCL_AMD_LIBDIR=${GRAFT_REPO_ROOT:-$PWD}/fscl_amd/_build_rehearsal
 CFG=$1; TAG=$2; MODE=$3; W=$4
 R=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$R/gpurun_out/simtp_$TAG
