@@ -64,11 +64,13 @@ constexpr int NWAVE = WG / 64;
 constexpr int SEG = FSCLG_SEG;     // terms per work segment
 constexpr int SEG_SPLIT = 1024;    // split cells (latency): finer segments spread over the members' waves
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
-constexpr int MAXSEG_W = (163841 / SEG_SPLIT + 2 + 31) / 32 * 32;  // segments per walk (163 at 163841 terms, split)
+constexpr int MAXSEG_W = (163841 / SEG_SPLIT + 4 + 31) / 32 * 32;  // segments per walk (165 at 163841 terms, split;
+                                                                  // each part's ends are 128-site aligned)
 constexpr int SEGWORDS = MAXSEG_W / 32;
 constexpr int MAXTIES = 512;       // per eval_walks; overflow sends the affected argmax to the exact slow path
 constexpr int MAXREF = 16;
 constexpr int LDS_WG = FSCLG_LDS_WG;  // LDS per workgroup (default: two workgroups per CU, 160 KiB)
+
 #ifndef FSCLG_U
 #define FSCLG_U 2
 #endif
@@ -85,6 +87,13 @@ constexpr int PAD = 1024;             // slack after pos/row: a trip may read up
 static_assert(2 * 64 * U_MAX <= PAD, "look-ahead past the padding");
 static_assert(SEG_SPLIT % (64 * U_SPLIT) == 0 && SEG % (64 * U_MAIN) == 0, "segments of whole trips");
 constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsigned order = signed order
+static_assert(U_MAIN == 2 && U_SPLIT == 2, "the interleaved site array holds two sites per lane per trip");
+
+// The site array is interleaved per aligned block of 128 sites (one trip): lane l's 16 bytes
+// hold sites l and l + 64 of the block, so a trip's sites are one dwordx4 per lane (one
+// vector-memory instruction where two dwordx2 cost two: the texture path takes ~16 cycles per
+// wave-instruction whatever its width, tools/vmem_probe).  Site i lives at phys(i).
+__host__ __device__ __forceinline__ uint32_t phys(uint32_t i) { return (i & ~127u) | ((i & 63u) << 1) | ((i >> 6) & 1u); }
 
 enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2, PF_SPLIT_TIMEOUT = 4 };
 
@@ -231,11 +240,12 @@ struct XAcc {
 // interval thresholds and the null rows (offsets in Params)
 extern __shared__ __attribute__((aligned(16))) char fsclg_dyn[];
 
-__device__ __forceinline__ uint2 ld_pr(const uint2* base, uint32_t i) {
-  return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(base) + (i << 3));
+// a trip's two sites of this lane: block bs (a multiple of 128), sites bs + lane, bs + 64 + lane
+__device__ __forceinline__ uint4 ld_trip(const uint2* base, uint32_t bs, int lane) {
+  return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(base) + ((bs + 2u * (uint32_t)lane) << 3));
 }
 
-__device__ __forceinline__ int pos_at(const Params& P, int i) { return (int)(P.pr[i].x ^ POS_BIAS); }
+__device__ __forceinline__ int pos_at(const Params& P, int i) { return (int)(P.pr[phys(i)].x ^ POS_BIAS); }
 
 // log of |d| as sm-search.c:40-46: three branches, each c_b + log_table[|d| >> 8b], merged
 // into one precomputed table (the host forms c_b + log_table[i] with the same IEEE add)
@@ -266,7 +276,7 @@ __device__ __forceinline__ uint32_t absdist(uint32_t upos, uint32_t usweep) {
 }
 
 __device__ __forceinline__ double log_ad_of(int i, int sweep, double la, const Params& P) {
-  return logt_dev(absdist(P.pr[i].x, (uint32_t)sweep ^ POS_BIAS), P.logt3) + la;
+  return logt_dev(absdist(P.pr[phys(i)].x, (uint32_t)sweep ^ POS_BIAS), P.logt3) + la;
 }
 
 // spline interval of sm-spline.c:52-54, (int)((x - LOG_AD_MIN) / step) clamped, without the
@@ -352,7 +362,7 @@ template <bool LDS>
 __device__ __forceinline__ double term_dev(int i, int sweep, double la, const Smem& S, const Params& P) {
   const double x = log_ad_of(i, sweep, la, P);
   const int iv = interval_of<LDS>(x, S, P);
-  const uint32_t r = P.pr[i].y;
+  const uint32_t r = P.pr[phys(i)].y;
   double2 a, b;
   coef_fetch<LDS>(r, iv, S, P, a, b);
   const double y = x * (a.x * x * x + a.y * x + b.x) + b.y;
@@ -453,7 +463,7 @@ __device__ __forceinline__ void walk_bounds_g(Smem& S, const Params& P, int tid,
   const Pt& pt = S.pt[act ? W.p : 0];
   const int near = pt.nearest;
   const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS, df = W.dfail;
-  auto outside = [&](int i) { return absdist(P.pr[i].x, usweep) >= df; };
+  auto outside = [&](int i) { return absdist(P.pr[phys(i)].x, usweep) >= df; };
   int lo = 0, hi = 1;
   bool ok1 = false;
   if (act) {
@@ -534,20 +544,34 @@ __device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, 
 
 // A walk covers the site indices [nearest - nl, nearest + nr]; its left part
 // [nearest - nl, nearest] (walked downwards, sm-search.c:122-128) and right part
-// [nearest + 1, nearest + nr] are cut into separate SEG-site segments (left ones first), so
-// each part's walk order is monotone in the index.
+// [nearest + 1, nearest + nr] are cut into separate segments (left ones first), so each
+// part's walk order is monotone in the index.  Segments lie on the aligned SEGN-site grid
+// that starts at the part's first 128-site block: interior boundaries are trip-aligned, and
+// only a part's first and last trips are partial (masked).
 template <int SEGN>
 __device__ __forceinline__ void seg_bounds(const Walk& W, const Pt& pt, int s, int& ib, int& ie) {
   const int lo = pt.nearest - W.nl, near = pt.nearest, hi = pt.nearest + W.nr;
-  if (s < W.nsl) { ib = lo + s * SEGN; ie = min(ib + SEGN, near + 1); }
-  else { ib = near + 1 + (s - W.nsl) * SEGN; ie = min(ib + SEGN, hi + 1); }
+  if (s < W.nsl) {
+    const int b0 = lo & ~127;
+    ib = max(lo, b0 + s * SEGN); ie = min(b0 + (s + 1) * SEGN, near + 1);
+  } else {
+    const int b1 = (near + 1) & ~127, t = s - W.nsl;
+    ib = max(near + 1, b1 + t * SEGN); ie = min(b1 + (t + 1) * SEGN, hi + 1);
+  }
+}
+
+// segments of a walk's two parts (layout)
+template <int SEGN>
+__device__ __forceinline__ void seg_counts(int lo, int near, int hi, int& nsl, int& nsr) {
+  nsl = (near - (lo & ~127)) / SEGN + 1;
+  nsr = hi > near ? (hi - ((near + 1) & ~127)) / SEGN + 1 : 0;
 }
 
 // the segment of site index i of the walk
 template <int SEGN>
 __device__ __forceinline__ int seg_of(const Walk& W, const Pt& pt, int i) {
   const int lo = pt.nearest - W.nl, near = pt.nearest;
-  return i <= near ? (i - lo) / SEGN : W.nsl + (i - near - 1) / SEGN;
+  return i <= near ? (i - (lo & ~127)) / SEGN : W.nsl + (i - ((near + 1) & ~127)) / SEGN;
 }
 
 __device__ __forceinline__ bool odd_int(double v) { return v - 2.0 * floor(0.5 * v) != 0.0; }
@@ -566,6 +590,18 @@ __device__ __forceinline__ double uniform_f64(double v) {
   const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+
+// FSCLG_TRIP_STAMPS (diagnostic build): per-trip phase times of the term loop, by s_memtime
+// stamps (each forces the waits before it): stats[8..23] = trips, then cycles in (nx wait +
+// |d|), (log distance + interval test), (coefficients + polynomial), (sums, ties, look-ahead),
+// trips per coefficient path (LDS, global, per lane) and the coefficient phase's cycles per
+// path, trips per log-distance path (LDS far, global mid, per lane) and the log phase's cycles
+// per path
+#ifdef FSCLG_TRIP_STAMPS
+#define TSTAMP(v) do { __builtin_amdgcn_sched_barrier(0); \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) :: "memory"); \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
+#endif
 
 // one index-order segment of one walk, by one wave, with a wave-uniform spline interval.  Along a segment
 // the sites move monotonically away from (or towards) the sweep, and a trip's 64*U sites
@@ -586,27 +622,36 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
   const int lo = pt.nearest - W.nl;
   int ib, ie;
   seg_bounds<SEGN>(W, pt, s, ib, ie);
-  int n = ie - ib;
+  // trips run over the aligned 128-site blocks from bs: sites bs + k, k in [k0, n), belong to
+  // the segment (lanes outside it take the zero sentinel row)
+  int bs = ib & ~127, k0 = ib - bs, n = ie - bs;
   const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
   const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
   int civ = 0;
   double sum = 0.0, mag = 0.0;
-  // the sites of the next trip are loaded one trip ahead (nx), issued after the trip's own
-  // coefficient loads so that waiting for a global coefficient gather (vmcnt counts in
-  // order) does not wait for them; PAD covers the look-ahead past a segment's end.  Segments
-  // [s, s1) of one part are contiguous: the look-ahead runs on into the next one
-  uint2 nx[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) nx[u] = ld_pr(P.pr, (uint32_t)(ib + 64 * u + lane));
+  // the sites of the next trip are loaded one trip ahead (nx, one dwordx4: sites bs + kb +
+  // lane and + 64 + lane of the interleaved array), issued after the trip's own coefficient
+  // loads so that waiting for a global coefficient gather (vmcnt counts in order) does not
+  // wait for them; PAD covers the look-ahead past a segment's end
+  uint4 nx = ld_trip(P.pr, (uint32_t)bs, lane);
+#ifdef FSCLG_TRIP_STAMPS
+  unsigned long long tsa[16] = {0};
+#endif
   auto trip = [&](const int kb, auto maskc) {
     constexpr bool MASK = decltype(maskc)::value;
+#ifdef FSCLG_TRIP_STAMPS
+    unsigned long long t_a, t_b, t_c, t_d, t_e;
+    int lpath = 2, cpath = 2;
+    TSTAMP(t_a);
+#endif
     uint32_t pv[U], rv[U];
+    bool valid[U];
+    pv[0] = nx.x; rv[0] = nx.y; pv[1] = nx.z; rv[1] = nx.w;
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int k = kb + 64 * u + lane;
-      const uint2 v = nx[u];
-      pv[u] = v.x;
-      rv[u] = (!MASK || k < n) ? v.y : 0u;  // zero sentinel row past the segment
+      valid[u] = !MASK || (k >= k0 && k < n);
+      if (!valid[u]) rv[u] = 0u;  // zero sentinel row outside the segment
     }
     // log distance: when every lane's |d| lies in the LDS copy of the far branch (one
     // unsigned compare per site: |d| in [2^24, lt_hi << 16)), straight from LDS; when every
@@ -624,6 +669,10 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
     bool mid = true;  // every |d| in the mid branch (2^16 <= |d| < 2^24): one global gather each
 #pragma unroll
     for (int u = 0; u < U; u++) mid = mid && (ad[u] - 0x10000u < 0xFF0000u);
+#ifdef FSCLG_TRIP_STAMPS
+    TSTAMP(t_b);
+    lpath = (LDS && __builtin_amdgcn_ballot_w64(far) == ~0ull) ? 0 : (__builtin_amdgcn_ballot_w64(mid) == ~0ull ? 1 : 2);
+#endif
     if (LDS && __builtin_amdgcn_ballot_w64(far) == ~0ull) {
       const double* lt2 = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt);  // pre-offset by -256 entries
 #pragma unroll
@@ -648,7 +697,7 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
 #pragma unroll
     for (int u = 0; u < U; u++) {
       if constexpr (MASK) {  // masked lanes add exactly 0 anyway
-        const bool ok = ((x[u] >= tlo) && (x[u] < thi)) || kb + 64 * u + lane >= n;
+        const bool ok = ((x[u] >= tlo) && (x[u] < thi)) || !valid[u];
         inm &= __builtin_amdgcn_ballot_w64(ok);
       } else {
         inm &= __builtin_amdgcn_ballot_w64(x[u] >= tlo) & __builtin_amdgcn_ballot_w64(x[u] < thi);
@@ -656,6 +705,10 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
     }
     const bool uni = inm == ~0ull;
     double2 ca[U], cb[U];
+#ifdef FSCLG_TRIP_STAMPS
+    TSTAMP(t_c);
+    cpath = !uni ? 2 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 0 : 1);
+#endif
 #ifdef FSCLG_PATHSTATS  // diagnostic: trips per path in the stats slots 4 (per-lane), 5 (LDS), 6 (global)
     if (lane == 0) atomicAdd(&S.cnt[!uni ? 4 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 5 : 6)], 1ull);
 #endif
@@ -682,12 +735,27 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
     // registers, no copy at the loop edge), unconditional (the last trip's look-ahead reads
     // the padding; a conditional load would make the waits below conservative at the join)
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < U; u++) nx[u] = ld_pr(P.pr, (uint32_t)(ib + kb + 64 * U + 64 * u + lane));
+    nx = ld_trip(P.pr, (uint32_t)(bs + kb + 128), lane);
     __builtin_amdgcn_sched_barrier(0);
+#ifdef FSCLG_TRIP_STAMPS
+    double yv[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) yv[u] = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
+    {
+      double yy = yv[0];
+#pragma unroll
+      for (int u = 1; u < U; u++) yy += yv[u];
+      asm volatile("" :: "v"(yy));
+    }
+    TSTAMP(t_d);
+#endif
 #pragma unroll
     for (int u = 0; u < U; u++) {
+#ifdef FSCLG_TRIP_STAMPS
+      const double y = yv[u];
+#else
       const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
+#endif
       const double q = (y - nul[u]) * inv;
       const double R = rint(q);                 // the even neighbour at a tie; the resolver settles ties
       const double fr = q - R;
@@ -699,26 +767,38 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
         if (fabs(fr) == 0.5) {
           const int ti = atomicAdd(&S.n_ties, 1);
           if (ti < MAXTIES)
-            S.ties[ti] = (w << 20) | ((fr < 0.0 ? 1 : 0) << 19) | (pre << 18) | (ib + kb + 64 * u + lane - lo);
+            S.ties[ti] = (w << 20) | ((fr < 0.0 ? 1 : 0) << 19) | (pre << 18) | (bs + kb + 64 * u + lane - lo);
         }
       }
       sum += R;
       mag += fabs(R);
     }
+#ifdef FSCLG_TRIP_STAMPS
+    asm volatile("" :: "v"(sum), "v"(mag));
+    TSTAMP(t_e);
+    tsa[0] += 1; tsa[1] += t_b - t_a; tsa[2] += t_c - t_b; tsa[3] += t_d - t_c; tsa[4] += t_e - t_d;
+    tsa[5 + cpath] += 1; tsa[8 + cpath] += t_d - t_c; tsa[11 + lpath] += 1;
+    if (lpath == 1) tsa[14] += t_c - t_b; else if (lpath == 0) tsa[15] += t_c - t_b;
+#endif
   };
   for (;;) {
     int kb = 0;
-    for (; kb + 64 * U <= n; kb += 64 * U) trip(kb, std::false_type{});
+    if (k0 > 0) { trip(0, std::true_type{}); kb = 128; }  // a part's first trip starts mid-block
+    for (; kb + 128 <= n; kb += 128) trip(kb, std::false_type{});
     if (kb < n) trip(kb, std::true_type{});
     const unsigned long long odd = __ballot(odd_int(sum));
     if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
+#ifdef FSCLG_TRIP_STAMPS
+    if (lane == 0)
+      for (int j = 0; j < 16; j++) atomicAdd(P.stats + 8 + j, tsa[j]);
+    for (int j = 0; j < 16; j++) tsa[j] = 0;
+#endif
     acc += sum;
     accm += mag;
     if (++s >= s1) break;
-    // the next segment of the part starts where this one ended (a full one: SEGN sites, a
-    // multiple of the trip, so the look-ahead already holds its first trip)
     seg_bounds<SEGN>(W, pt, s, ib, ie);
-    n = ie - ib;
+    bs = ib & ~127; k0 = ib - bs; n = ie - bs;
+    nx = ld_trip(P.pr, (uint32_t)bs, lane);
     sum = 0.0; mag = 0.0;
   }
 }
@@ -999,7 +1079,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
       const int near = S.pt[W.p].nearest, lo = near - W.nl, hi = near + W.nr;
       int nsl;
       if (!len) { nsl = 0; nseg = 0; }
-      else { nsl = (W.nl + SEGN) / SEGN; nseg = nsl + (W.nr + SEGN - 1) / SEGN; }
+      else { int nsr; seg_counts<SEGN>(lo, near, hi, nsl, nsr); nseg = nsl + nsr; }
       W.len = len; W.wb = wb; W.nsl = nsl; W.nseg = nseg;
     }
     // walks in descending window base, stable: each walk's rank and first segment
@@ -1430,11 +1510,11 @@ window_null_kernel(const uint2* __restrict__ pr, const double* __restrict__ null
     if (T1 - T0 == WN_TILE) {
       uint32_t rr[WN_TILE / WN_WG];
 #pragma unroll
-      for (int q = 0; q < WN_TILE / WN_WG; q++) rr[q] = pr[T0 + k + q * WN_WG].y;
+      for (int q = 0; q < WN_TILE / WN_WG; q++) rr[q] = pr[phys((uint32_t)(T0 + k + q * WN_WG))].y;
 #pragma unroll
       for (int q = 0; q < WN_TILE / WN_WG; q++) tile[k + q * WN_WG] = nullrow[rr[q]];
     } else {
-      for (int j = T0 + k; j < T1; j += WN_WG) tile[j - T0] = nullrow[pr[j].y];
+      for (int j = T0 + k; j < T1; j += WN_WG) tile[j - T0] = nullrow[pr[phys((uint32_t)j)].y];
     }
     __syncthreads();
     if (nwin == 0) continue;
@@ -1474,7 +1554,7 @@ window_null_kernel(const uint2* __restrict__ pr, const double* __restrict__ null
     if (m < nwin) out[base + m] = a[m];
 }
 
-// one trial's rows into the (position, row) array: pr[i].y = row[i] + 1 (device row), read
+// one trial's rows into the (position, row) array: pr[phys(i)].y = row[i] + 1 (device row), read
 // straight from the pinned host staging (no copy-engine transfer, which would order this
 // stream's work behind other streams' copies); block 0 also takes the whole-chromosome null
 // sums.  row == null: the uploaded rows (pr0).
@@ -1488,12 +1568,13 @@ __global__ void __launch_bounds__(256) scatter_rows_kernel(uint2* __restrict__ p
   if (i + 3 < n) {
     if (row) {
       const uint4 r4 = *reinterpret_cast<const uint4*>(row + i);
-      pr[i].y = r4.x + 1u; pr[i + 1].y = r4.y + 1u; pr[i + 2].y = r4.z + 1u; pr[i + 3].y = r4.w + 1u;
+      pr[phys(i)].y = r4.x + 1u; pr[phys(i + 1)].y = r4.y + 1u; pr[phys(i + 2)].y = r4.z + 1u;
+      pr[phys(i + 3)].y = r4.w + 1u;
     } else {
-      for (int k = 0; k < 4; k++) pr[i + k].y = pr0[i + k].y;
+      for (int k = 0; k < 4; k++) pr[phys(i + k)].y = pr0[phys(i + k)].y;
     }
   } else {
-    for (int k = i; k < n; k++) pr[k].y = row ? row[k] + 1u : pr0[k].y;
+    for (int k = i; k < n; k++) pr[phys(k)].y = row ? row[k] + 1u : pr0[phys(k)].y;
   }
   if (blockIdx.x == 0 && chr_null_src)
     for (int c = threadIdx.x; c < n_chr; c += 256) chr_null[c] = chr_null_src[c];
@@ -1708,8 +1789,8 @@ int fsclg_open(int device, fsclg_ctx** out) {
   HIPCHK(hipEventCreate(&c->ev_ref), "hipEventCreate");
   HIPCHK(hipEventCreate(&c->wev0), "hipEventCreate");
   HIPCHK(hipEventCreate(&c->wev1), "hipEventCreate");
-  HIPCHK(hipMalloc((void**)&c->d_stats, sizeof(unsigned long long) * 8), "hipMalloc stats");
-  HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
+  HIPCHK(hipMalloc((void**)&c->d_stats, sizeof(unsigned long long) * 24), "hipMalloc stats");  // 8 + FSCLG_TRIP_STAMPS
+  HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 24), "hipMemset");
   HIPCHK(hipEventRecord(c->ev_ref, c->ustream), "hipEventRecord");
   HIPCHK(hipEventSynchronize(c->ev_ref), "hipEventSynchronize");
   *out = c;
@@ -1809,9 +1890,10 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
     if (c->n_rows && row[i] >= (uint32_t)c->n_rows) return set_err(FSCLG_E_ARG, "row index out of table");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
-  // PAD slack after both arrays (zeros: a valid position and row, never counted)
-  std::vector<uint2> pr((size_t)n_snps + PAD, make_uint2(POS_BIAS, 0u));
-  for (int i = 0; i < n_snps; i++) pr[i] = make_uint2((uint32_t)pos[i] ^ POS_BIAS, row[i] + 1);
+  // interleaved per 128-site block (phys), rounded up to whole blocks, then PAD slack (zeros:
+  // a valid position and row, never counted)
+  std::vector<uint2> pr(((size_t)n_snps + 127) / 128 * 128 + PAD, make_uint2(POS_BIAS, 0u));
+  for (int i = 0; i < n_snps; i++) pr[phys((uint32_t)i)] = make_uint2((uint32_t)pos[i] ^ POS_BIAS, row[i] + 1);
   if ((r = upload(&c->d_pr0, pr.data(), pr.size(), c->ustream))) return r;
   for (Slot& S : c->slot) {
     if ((r = upload(&S.d_pr, pr.data(), pr.size(), c->ustream))) return r;
@@ -1838,8 +1920,9 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   }
   c->h_row_cnt.clear();
   for (int i = 0; i < n_snps; i++) {
-    if (pr[i].y >= c->h_row_cnt.size()) c->h_row_cnt.resize(pr[i].y + 1, 0);
-    c->h_row_cnt[pr[i].y]++;
+    const uint32_t dr = row[i] + 1;
+    if (dr >= c->h_row_cnt.size()) c->h_row_cnt.resize(dr + 1, 0);
+    c->h_row_cnt[dr]++;
   }
   c->h_pr0.swap(pr);
   c->plan_dirty = true;
@@ -2381,7 +2464,7 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
   for (int i = 0; i < n_cells; i++) {
     if (cells[i].chr < 0 || cells[i].chr >= c->n_chr) return set_err(FSCLG_E_ARG, "cell chromosome");
     const long long nwin = std::min((long long)c->h_chr_n[cells[i].chr], 2ll * eval_range + 1);
-    if (nwin / SEG_SPLIT + 2 > (long long)MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
+    if (nwin / SEG_SPLIT + 4 > (long long)MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
   }
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
@@ -2634,9 +2717,10 @@ int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
   // which needs no co-residency and gives the same results
   bool retry = false;
   for (int i = 0; i < B.n_cells && !retry; i++) retry = (out[i].flags & PF_SPLIT_TIMEOUT) && B.split > 1;
-  {  // FSCLG_FORCE_SPLIT_RETRY=n (tests): treat the first n split launches as timed out
-    static int forced = getenv("FSCLG_FORCE_SPLIT_RETRY") ? atoi(getenv("FSCLG_FORCE_SPLIT_RETRY")) : 0;
-    if (!retry && B.split > 1 && forced > 0) { forced--; retry = true; }
+  {  // FSCLG_FORCE_SPLIT_RETRY=n (tests): treat split launches as timed out until n retries were
+     // counted since the last fsclg_reset_stats
+    const char* fe = getenv("FSCLG_FORCE_SPLIT_RETRY");
+    if (!retry && B.split > 1 && fe && c->n_split_retry < (unsigned long long)atoll(fe)) retry = true;
   }
   if (retry) {
     std::vector<fsclg_cell_t> cells(B.n_cells);
@@ -2684,7 +2768,7 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
     if (p.window_start < 0 || p.window_end >= c->n_snps || p.window_start > p.window_end ||
         p.nearest_snp < p.window_start || p.nearest_snp > p.window_end)
       return set_err(FSCLG_E_ARG, "point window");
-    if ((p.window_end - p.window_start + 1) / SEG_SPLIT + 2 > MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
+    if ((p.window_end - p.window_start + 1) / SEG_SPLIT + 4 > MAXSEG_W) return set_err(FSCLG_E_UNSUPPORTED, "window above the segment table");
   }
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   int r;
@@ -2746,6 +2830,19 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
   unsigned long long h[8];
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost), "copy stats");
+#ifdef FSCLG_TRIP_STAMPS
+  {
+    unsigned long long t[16];
+    HIPCHK(hipMemcpy(t, c->d_stats + 8, sizeof t, hipMemcpyDeviceToHost), "copy stamps");
+    const double n = t[0] ? (double)t[0] : 1.0;
+    fprintf(stderr, "[trip stamps] trips %llu  cycles/trip: nx+|d| %.0f  log+interval %.0f  coef+poly %.0f  sums %.0f\n"
+                    "  coef path trips LDS %llu global %llu per-lane %llu; coef+poly cycles/trip %.0f / %.0f / %.0f\n"
+                    "  log path trips LDS-far %llu mid %llu per-lane %llu; log+interval cycles/trip mid %.0f far %.0f\n",
+            t[0], t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5], t[6], t[7], t[8] / (t[5] ? (double)t[5] : 1.0),
+            t[9] / (t[6] ? (double)t[6] : 1.0), t[10] / (t[7] ? (double)t[7] : 1.0), t[11], t[12], t[13],
+            t[14] / (t[12] ? (double)t[12] : 1.0), t[15] / (t[11] ? (double)t[11] : 1.0));
+  }
+#endif
   memset(st, 0, sizeof *st);
   st->n_terms = h[0]; st->n_null = h[1]; st->n_walks = h[2]; st->n_maxalpha = h[3];
   st->n_unsafe = h[4]; st->n_slow = h[5]; st->n_ties = h[6]; st->n_cells = h[7];
@@ -2772,7 +2869,7 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
 int fsclg_reset_stats(fsclg_ctx* c) {
   if (!c) return set_err(FSCLG_E_ARG, "stats");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
-  HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 8), "hipMemset");
+  HIPCHK(hipMemset(c->d_stats, 0, sizeof(unsigned long long) * 24), "hipMemset");
   for (int k = 0; k < NSLOT; k++) window_time(c, c->slot[k]);  // pending times belong before the reset
   c->kernel_ms = 0.0; c->launches = 0; c->window_ms = 0.0; c->n_dup_cells = 0; c->n_ep_saved = 0; c->n_split_retry = 0;
   c->busy.clear();
