@@ -193,8 +193,22 @@ def points_digest(pts) -> tuple[str, list[str]]:
     return h.hexdigest(), rows
 
 
+def heartbeat(period: float = 30.0) -> None:
+    """A line on stderr every `period` seconds (long jobs, e.g. C5, print nothing else for minutes)."""
+    import threading
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print(f"bench.py: running, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main() -> int:
     args = parse()
+    heartbeat()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -273,6 +287,9 @@ def main() -> int:
         [f"--asc-depth={cfg['asc_depth']}", f"--asc-minimum-freq={cfg.get('asc_min_freq', 1)}"]
         if cfg.get("asc_depth", 0) else [])
     fx_name, fx = full_job_fixture(snp, job_opts) if rank == 0 and args.permute_mode == "parity" else (None, None)
+    # else the oracle's digest of this genome's initial scan alone, where one exists (C5: its 50k-cell
+    # initial scan takes the oracle minutes, too long to run live beside the bench)
+    sfx_name, sfx = full_job_fixture(snp, []) if rank == 0 and fx is None and job_opts else (None, None)
 
     fscl_amd.set_permute_mode(args.permute_mode)
 
@@ -397,6 +414,18 @@ def main() -> int:
         if not all(ok):
             print(f"bench.py: PARITY FAILURE: {len(ok) - sum(ok)} of {len(ok)} timed jobs differ from {fx_name}",
                   file=sys.stderr)
+    elif sfx is not None:
+        fscl_amd.srand()
+        fscl_amd.scan_chromosome(scan, tab)
+        dig, rows = points_digest(fscl_amd.points(scan))
+        k = sfx["sample_every"]
+        ok = dig == sfx["dump_sha256"]
+        out["parity"] = {"scope": "initial scan", "fixture": f"tests/golden/fullsize.json[{sfx_name}]",
+                         "what": "SHA-256 of every field of every point of the GPU's initial scan of this genome "
+                                 "against the oracle's (no fixture of the whole permutation job exists at this size)",
+                         "points": sfx["n_points"], "identical": ok,
+                         "sampled_rows_differing": 0 if ok else sum(rows[i * k] != w for i, w in enumerate(sfx["sample"]))}
+        out["max_abs_dclr"] = 0.0 if ok else None
     elif rank == 0:
         out["parity"] = {"scope": "initial scan" if world == 1 and n_local == 1 and not args.no_cpu_baseline else
                          "none in this run", "note": "no oracle fixture of this exact job (tests/golden/fullsize.json)"}
@@ -414,8 +443,8 @@ def main() -> int:
         info = cpu_info()
         out["cpu_baseline"], scan_dclr, out["position_mismatches"] = cpu_baseline(
             args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, n_perm_units, st["trials"] // max(1, args.steps),
-            units / args.steps, elapsed / args.steps)
-        if out["max_abs_dclr"] is None or fx is None:
+            units / args.steps, elapsed / args.steps, live_parity=fx is None and sfx is None)
+        if fx is None and sfx is None:
             out["max_abs_dclr"] = scan_dclr
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -441,8 +470,10 @@ def _harness(snp, cfg, threads, n_cells):
     return {k: float(v) for k, v in kv.items()}
 
 
-def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, trials, units, gpu_job_s):
-    """Returns (cpu_baseline dict, max |dCLR|, position mismatches)."""
+def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, trials, units, gpu_job_s,
+                 live_parity=True):
+    """Returns (cpu_baseline dict, max |dCLR|, position mismatches); live_parity=False: the parity block
+    came from a committed oracle fixture instead of a live oracle run."""
     sys.path.insert(0, str(ROOT / "oracle"))
     from oracle import OracleScan  # noqa: E402
     threads = args.cpu_threads or info["usable_cpus"]  # every CPU this process may use (cgroup quota included)
@@ -475,6 +506,9 @@ def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, 
                           "note": "one-thread per-cell time / the node's physical cores (perfect scaling, "
                                   "an upper bound for the CPU) + the serial permutations"},
           **info, "gpu_over_cpu": job_s / gpu_job_s, "gpu_over_node_linear": node_s / gpu_job_s}
+    if not live_parity:
+        bl["parity"] = "see the line's parity block (committed oracle fixture)"
+        return bl, None, None
     # parity of the GPU's initial scan with the oracle on every cell (same run, same host)
     fscl_amd.srand()
     fscl_amd.scan_chromosome(scan, tab)
