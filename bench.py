@@ -333,23 +333,45 @@ def main() -> int:
     alg_gbs = alg_bytes / busy_s / 1e9 if busy_s > 0 else 0.0
     prof, prof_src = profile_summary(args)
     traffic = prof.get("hbm_bytes_per_launch") if prof else None
-    roof = issue_roofline(prof) if prof else None
-    if roof is None:  # no committed PMC for this config: the algorithmic-byte figure alone
-        roof = {"bound": "unmeasured", "achieved": alg_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": alg_gbs / HBM_PEAK_GBS}
-    roof.update({
-        "traffic": traffic, "source": prof_src, "kernel": "search_maxpos_kernel",
-        "alg_bytes_per_launch": alg_bytes / launches,
-        "alg_gbs": alg_gbs, "alg_frac": alg_gbs / HBM_PEAK_GBS,
-        "traffic_over_alg": (traffic / (alg_bytes / launches)) if traffic and alg_bytes else None,
-        "hbm_frac": (traffic * launches / busy_s / 1e9 / HBM_PEAK_GBS) if traffic and busy_s > 0 else None,
-        "avg_launch_ms": st["kernel_ms"] / launches, "launches": st["n_launches"], "busy_ms": st["busy_ms"],
-        "terms_per_s": st["n_terms"] / busy_s if busy_s > 0 else 0.0,
-        "note": "bound from measurement (DESIGN.md §4.6): the kernel is latency/issue-bound -- achieved/frac = "
-                "VALU issue cycles (committed rocprofv3 PMC, source) over the SIMD-cycles of the launches; "
-                "alg_gbs/alg_frac = SURVEY 8(d)'s algorithmic bytes (8 B per SNP term and per window-null "
-                "element) over the launches' union (live HIP events); traffic = measured HBM bytes per launch "
-                "(FETCH_SIZE x2 + WRITE_SIZE): sites, tables and coefficient windows stay in L2/LDS"})
+    issue = issue_roofline(prof) if prof else None
+    # FETCH_SIZE sanity: bytes per launch over the counter pass's own (serialized) dispatch time must
+    # stay under the memory system's rates; C5's search dispatches report values that imply PB/s
+    # (a counter artefact), and those are not used
+    traffic_note = None
+    if traffic and prof.get("pmc_dispatch_ms", {}).get("fetch"):
+        implied = traffic / (prof["pmc_dispatch_ms"]["fetch"] * 1e-3) / 1e9
+        if implied > 2 * HBM_PEAK_GBS:
+            traffic_note = (f"FETCH_SIZE of this profile implies {implied / 1e3:.0f} TB/s over the dispatches' own "
+                            f"duration, above any memory rate: a counter artefact, not used")
+            traffic = None
+    mem = None
+    mem_path = ROOT / "profiles" / "r03b_pmc_mem_c4_c2.json"
+    if mem_path.exists() and args.config.lower() in ("c4", "c2"):
+        m = json.loads(mem_path.read_text())[args.config.lower()]
+        t = m["totals_over_job"]
+        mem = {"source": str(mem_path.relative_to(ROOT)), **{k: round(v, 3) for k, v in m["per_term"].items()},
+               "tcc_hit_rate": t["TCC_HIT_sum"] / max(1.0, t["TCC_HIT_sum"] + t["TCC_MISS_sum"])}
+    # SURVEY 8(d)'s roofline: algorithmic bytes (8 B per SNP term and per window-null element) per launch
+    # over the launches' busy union (live HIP events on the batches' own streams), against HBM peak.
+    roof = {"bound": "hbm", "achieved": alg_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg_gbs / HBM_PEAK_GBS,
+            "traffic": traffic, "traffic_note": traffic_note, "source": prof_src, "kernel": "search_maxpos_kernel",
+            "alg_bytes_per_launch": alg_bytes / launches,
+            "traffic_over_alg": (traffic / (alg_bytes / launches)) if traffic and alg_bytes else None,
+            "hbm_frac": (traffic * launches / busy_s / 1e9 / HBM_PEAK_GBS) if traffic and busy_s > 0 else None,
+            "avg_launch_ms": st["kernel_ms"] / launches, "launches": st["n_launches"], "busy_ms": st["busy_ms"],
+            "busy_ms_per_launch": st["busy_ms"] / launches,
+            "rocprof_avg_launch_ms": prof.get("trace", {}).get("avg_ms") if prof else None,
+            "rocprof_busy_ms_per_launch": prof.get("trace_union", {}).get("busy_ms_per_launch") if prof else None,
+            "terms_per_s": st["n_terms"] / busy_s if busy_s > 0 else 0.0,
+            # what actually limits it: not HBM (real traffic is a few % of the algorithmic
+            # bytes: sites, tables and coefficient windows stay in L2/LDS) and not issue (VALU issue below
+            # half its peak): latency of the dependent L2 gathers per trip, waves parked on memory
+            "limiter": "latency" if issue else "unmeasured",
+            "issue": issue, "memory_path": mem,
+            "note": "achieved/frac: SURVEY 8(d) algorithmic bytes over the launches' union; limiter from the "
+                    "committed rocprofv3 PMC of this workload (source): VALU issue (issue.frac), waves waiting on "
+                    "memory (issue.wait_any_frac), texture-path cycles per term (memory_path); traffic = measured "
+                    "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)"}
 
     out = {
         "metric": METRIC,

@@ -1,26 +1,30 @@
 // fsclg.hip -- gfx950 kernels for fscl's CLR sweep scan (search_maxpos batch).
 //
-// One 512-thread workgroup (8 wave64s) owns one coarse grid cell and runs the
-// whole position bisection of scan-chromosome.c:103-139 on chip: init of the
-// start/end/mid points (init_scan_result, :58-101), and for each point the
-// alpha search of sm-search.c:269-300 as two phases (11 coarse, 14-15 refine
-// candidates).  A phase evaluates every candidate's bidirectional walk
-// (sm-search.c:105-150) as a contiguous index range found by binary search
-// (log(alpha*d) is monotone in |d|), splits the walks into 1024-term segments
-// that the 8 waves pull from an LDS counter, and sums each walk EXACTLY as the
-// reference's sequential `sm_logl += term` would, in any order:
+// One 768-thread workgroup (12 wave64s; two workgroups per CU, 6 waves per SIMD, 80 KB of LDS
+// each) owns one coarse grid cell and runs the whole position bisection of
+// scan-chromosome.c:103-139 on chip: the cell's end points (init_scan_result, :58-101), and
+// for each point the alpha search of sm-search.c:269-300 as two phases (11 coarse, 14-15
+// refine candidates), two bisection levels per alpha search.  A phase evaluates every
+// candidate's bidirectional walk (sm-search.c:105-150) as a contiguous index range found by a
+// wave-parallel search (log(alpha*d) is monotone in |d|), cuts each walk part into 4096-site
+// segments on the aligned 128-site trip grid, deals the segments round-robin to the 12 waves
+// (a trip: 128 sites, two per lane, one dwordx4 load of the interleaved site array), and sums
+// each walk EXACTLY as the reference's sequential `sm_logl += term` would, in any order:
 //
-//   inside the binade of the start value N (the window null sum) every
-//   sequential add is  S += rne(t/u)  with u = ulp(N), an integer; ties
-//   (t/u = F + 1/2) round to the even running sum, so each tie needs only the
-//   PARITY of the prefix, which is a popcount of ballots.  Per lane: int64
-//   sums of the positive / negative parts; per segment: a parity bit; per tie:
-//   its in-segment prefix parity.  A walk whose partial sums may leave the
-//   binade is "unsafe": it gets a rigorous approximation + error bound, and is
-//   re-summed sequentially only if it could be the argmax (never observed).
+//   inside the binade of the start value N (the window null sum) every sequential add is
+//   S += rne(t/u) with u = ulp(N), an integer; ties (t/u = F + 1/2) round to the even running
+//   sum, so each tie needs only the PARITY of the prefix, which is a popcount of ballots.
+//   Per lane: fp64 sums of R = rint(t/u) and of |R| (exact below 2^51); per segment: a parity
+//   bit; per tie: its in-segment prefix parity.  A walk whose partial sums may leave the
+//   binade gets a rigorous approximation + error bound, and is re-summed sequentially only if
+//   it could be the argmax.
 //
-// Arithmetic is compiled with contraction off (no FMA fusing): the reference's
-// polynomial and log(alpha d) adds are reproduced operation for operation.
+// Few-cell launches (the permutation pipeline's blocking batches, the drop-in search_maxalpha)
+// give each cell up to 8 workgroups ("split cells") that share the walks' segments and combine
+// their sums through per-cell agent-scope exchange areas.
+//
+// Arithmetic is compiled with contraction off (no FMA fusing): the reference's polynomial and
+// log(alpha d) adds are reproduced operation for operation.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>

@@ -12,9 +12,10 @@ from pathlib import Path
 
 src, dst = Path(sys.argv[1]), sys.argv[2]
 Path(dst).parent.mkdir(parents=True, exist_ok=True)
-shutil.copy(src / "trace" / "run_kernel_stats.csv", f"{dst}_kernel_stats.csv")
+if (src / "trace" / "run_kernel_stats.csv").exists():
+    shutil.copy(src / "trace" / "run_kernel_stats.csv", f"{dst}_kernel_stats.csv")
 out = {"kernel": "search_maxpos_kernel"}
-for row in csv.DictReader(open(src / "trace" / "run_kernel_stats.csv")):
+for row in (csv.DictReader(open(src / "trace" / "run_kernel_stats.csv")) if (src / "trace" / "run_kernel_stats.csv").exists() else []):
     if "search_maxpos" in row["Name"]:
         out["trace"] = {"calls": int(row["Calls"]), "avg_ms": float(row["AverageNs"]) / 1e6,
                         "min_ms": float(row["MinNs"]) / 1e6, "max_ms": float(row["MaxNs"]) / 1e6,

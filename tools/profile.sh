@@ -21,4 +21,10 @@ for p in ${PASSES:-trace fetch write sq f64}; do
   echo "[profile] $p $(date +%T)"
   timeout -k 10 $LIM rocprofv3 $args --output-format csv -d $OUT/$p -o run -- python3 $R/bench.py "$@" > $OUT/bench_$p.json 2> $OUT/$p.err
 done
+# REDUCE=1: summarize on the box (tools/prof_summary.py) and drop the raw CSVs, which for a long job exceed
+# what a call may bring back; partial summaries of separate calls merge with tools/prof_merge.py
+if [ -n "$REDUCE" ]; then
+  python3 $R/tools/prof_summary.py $OUT $OUT/partial_$(echo ${PASSES:-all} | tr ' ' '_') > /dev/null
+  for p in ${PASSES:-trace fetch write sq f64}; do rm -rf $OUT/$p; done
+fi
 echo done
