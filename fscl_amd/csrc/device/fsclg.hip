@@ -91,7 +91,7 @@ constexpr int PAD = 1024;             // slack after pos/row: a trip may read up
 static_assert(2 * 64 * U_MAX <= PAD, "look-ahead past the padding");
 static_assert(SEG_SPLIT % (64 * U_SPLIT) == 0 && SEG % (64 * U_MAIN) == 0, "segments of whole trips");
 constexpr uint32_t POS_BIAS = 0x80000000u;  // positions are stored biased: unsigned order = signed order
-static_assert(U_MAIN == 2 && U_SPLIT == 2, "the interleaved site array holds two sites per lane per trip");
+static_assert(U_MAIN % 2 == 0 && U_SPLIT % 2 == 0, "the interleaved site array holds two sites per lane per block");
 
 // The site array is interleaved per aligned block of 128 sites (one trip): lane l's 16 bytes
 // hold sites l and l + 64 of the block, so a trip's sites are one dwordx4 per lane (one
@@ -637,7 +637,9 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
   // lane and + 64 + lane of the interleaved array), issued after the trip's own coefficient
   // loads so that waiting for a global coefficient gather (vmcnt counts in order) does not
   // wait for them; PAD covers the look-ahead past a segment's end
-  uint4 nx = ld_trip(P.pr, (uint32_t)bs, lane);
+  uint4 nx[U / 2];
+#pragma unroll
+  for (int j = 0; j < U / 2; j++) nx[j] = ld_trip(P.pr, (uint32_t)(bs + 128 * j), lane);
 #ifdef FSCLG_TRIP_STAMPS
   unsigned long long tsa[16] = {0};
 #endif
@@ -650,7 +652,8 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
 #endif
     uint32_t pv[U], rv[U];
     bool valid[U];
-    pv[0] = nx.x; rv[0] = nx.y; pv[1] = nx.z; rv[1] = nx.w;
+#pragma unroll
+    for (int j = 0; j < U / 2; j++) { pv[2 * j] = nx[j].x; rv[2 * j] = nx[j].y; pv[2 * j + 1] = nx[j].z; rv[2 * j + 1] = nx[j].w; }
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int k = kb + 64 * u + lane;
@@ -739,7 +742,8 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
     // registers, no copy at the loop edge), unconditional (the last trip's look-ahead reads
     // the padding; a conditional load would make the waits below conservative at the join)
     __builtin_amdgcn_sched_barrier(0);
-    nx = ld_trip(P.pr, (uint32_t)(bs + kb + 128), lane);
+#pragma unroll
+    for (int j = 0; j < U / 2; j++) nx[j] = ld_trip(P.pr, (uint32_t)(bs + kb + 64 * U + 128 * j), lane);
     __builtin_amdgcn_sched_barrier(0);
 #ifdef FSCLG_TRIP_STAMPS
     double yv[U];
@@ -787,8 +791,8 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
   };
   for (;;) {
     int kb = 0;
-    if (k0 > 0) { trip(0, std::true_type{}); kb = 128; }  // a part's first trip starts mid-block
-    for (; kb + 128 <= n; kb += 128) trip(kb, std::false_type{});
+    if (k0 > 0) { trip(0, std::true_type{}); kb = 64 * U; }  // a part's first trip starts mid-block
+    for (; kb + 64 * U <= n; kb += 64 * U) trip(kb, std::false_type{});
     if (kb < n) trip(kb, std::true_type{});
     const unsigned long long odd = __ballot(odd_int(sum));
     if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][s >> 5], 1u << (s & 31));
@@ -802,7 +806,8 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
     if (++s >= s1) break;
     seg_bounds<SEGN>(W, pt, s, ib, ie);
     bs = ib & ~127; k0 = ib - bs; n = ie - bs;
-    nx = ld_trip(P.pr, (uint32_t)bs, lane);
+#pragma unroll
+    for (int j = 0; j < U / 2; j++) nx[j] = ld_trip(P.pr, (uint32_t)(bs + 128 * j), lane);
     sum = 0.0; mag = 0.0;
   }
 }
