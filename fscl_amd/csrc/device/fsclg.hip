@@ -31,6 +31,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <cmath>
 #include <vector>
 #include <algorithm>
 #include <type_traits>
@@ -1492,6 +1493,7 @@ search_maxpos_split_kernel(Params P) {
 // read once from LDS feeds all of them, each accumulator in its own ascending order); the
 // block stages the elements its 1024 windows span through an LDS tile.
 constexpr int WN_WG = 256, WN_PER = 4, WN_TILE = 4096;
+constexpr int WC_MAXROWS = 4096;  // window_chunk_kernel's LDS copy of the null rows (larger tables: the sequential kernel)
 
 // A block's staging of a tile is one round of independent row loads (all of a full tile's rows
 // before any null value), and its sums read the tile eight elements at a time before adding
@@ -1563,6 +1565,128 @@ window_null_kernel(const uint2* __restrict__ pr, const double* __restrict__ null
     if (m < nwin) out[base + m] = a[m];
 }
 
+// ------------------------------------------------ window null sums by exact chunks
+// The same sums (acc = 0.0; acc += null_logl[i], i = ws..ws+W-1, sequentially) with most of the
+// 2 er + 1 dependent adds replaced by one step per aligned 64-site chunk.
+// While the running sum S stays in one binade, |S| in [2^e, 2^(e+1)), every sequential add rounds
+// to the grid u = 2^(e-52): with S = m u (m an integer, |m| in [2^52, 2^53)) and q = v / u
+// (exact: a power-of-two scaling), fl(S + v) = (m + rint(q)) u, except at a tie (q = F + 1/2),
+// which rounds to the even neighbour: m + F + ((m + F) & 1).  After a tie m is even, so a chunk's
+// total increment depends on S only through the parity of m on entry: two integers per (chunk,
+// binade), chunk_table_kernel.  Null values are log-probabilities (<= 0), so the partial sums are
+// monotone and a chunk stays in the binade iff its end does; a chunk that crosses into the next
+// binade, one holding a positive or non-finite value (NaN in the table), the windows' ends and
+// the first sites (until |S| >= 2^emin, where a binade spans at least a chunk) are added site by
+// site in order.  Same result as the sequential chain, bit for bit, for every window.
+constexpr int WC = 64;  // chunk length, aligned to the site index
+
+// chunk c, binade e = emin + k: tab[(c ne + k) 2 + p] = the integer increment of m over the
+// chunk's 64 sequential adds for an even (p = 0) or odd (p = 1) m on entry, as an exact double
+// (|increment| < 2^52 by the choice of emin); NaN when the chunk holds a value that is positive,
+// not finite, or lies past the last site
+__global__ void __launch_bounds__(256) chunk_table_kernel(const uint2* __restrict__ pr,
+                                                          const double* __restrict__ nullrow, int n_snps, int emin,
+                                                          int ne, double* __restrict__ tab) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int nch = (n_snps + WC - 1) / WC;
+  if (t >= nch * ne) return;
+  const int c = t / ne, k = t - c * ne;
+  const int e = emin + k;
+  double* o = tab + ((size_t)c * ne + k) * 2;
+  const double nan = __longlong_as_double(0x7FF8000000000000ll);
+  if ((c + 1) * WC > n_snps) { o[0] = nan; o[1] = nan; return; }
+  const double sc = __longlong_as_double((long long)(1023 + 52 - e) << 52);  // 2^(52 - e), e <= 52
+  long long d0 = 0, d1 = 0;
+  int p0 = 0, p1 = 1;
+  bool ok = true;
+  for (int j = 0; j < WC; j++) {
+    const double v = nullrow[pr[phys((uint32_t)(c * WC + j))].y];
+    if (!(v <= 0.0) || v == -__builtin_inf()) { ok = false; break; }  // positive, NaN or -inf
+    const double q = v * sc;
+    const double F = floor(q);
+    const long long Fi = (long long)F;
+    if (q - F == 0.5) {
+      d0 += Fi + ((p0 + Fi) & 1); p0 = 0;
+      d1 += Fi + ((p1 + Fi) & 1); p1 = 0;
+    } else {
+      const long long R = (long long)rint(q);
+      d0 += R; p0 = (int)((p0 + R) & 1);
+      d1 += R; p1 = (int)((p1 + R) & 1);
+    }
+  }
+  o[0] = ok ? (double)d0 : nan;
+  o[1] = ok ? (double)d1 : nan;
+}
+
+// one window per thread, 256 consecutive window starts per block (tasks: [start, count])
+__global__ void __launch_bounds__(WN_WG)
+window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nullrow, int n_rows1,
+                    const int2* __restrict__ tasks, int W, int emin, int ne, const double* __restrict__ tab,
+                    double* __restrict__ out) {
+  __shared__ double nul[WC_MAXROWS];
+  __builtin_amdgcn_s_setprio(2);  // beside the search kernels' waves, which wait on memory
+  for (int r = threadIdx.x; r < n_rows1; r += WN_WG) nul[r] = nullrow[r];
+  __syncthreads();
+  const int2 t = tasks[blockIdx.x];
+  if ((int)threadIdx.x >= t.y) return;
+  const int ws = t.x + (int)threadIdx.x, end = ws + W;
+  double s = 0.0;
+  // sites [i, i + n) added in order, their rows loaded eight at a time
+  auto elems = [&](int i, int n) {
+    for (int b = 0; b < n; b += 8) {
+      uint32_t rr[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) rr[q] = b + q < n ? pr[phys((uint32_t)(i + b + q))].y : 0u;
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+        if (b + q < n) s += nul[rr[q]];
+    }
+  };
+  // head: site by site until |S| >= 2^emin at a chunk boundary
+  const double lim = -__longlong_as_double((long long)(1023 + emin) << 52);  // -2^emin
+  int i = ws;
+  while (i < end) {
+    const int n = min(WC - (i & (WC - 1)), end - i);  // to the next chunk boundary
+    if ((i & (WC - 1)) == 0 && s <= lim) break;
+    elems(i, n);
+    i += n;
+  }
+  // chunks, in batches of WCB: the batch's table entries for the running binade are loaded together
+  // (one load latency per batch, not per chunk), then applied in order until a chunk would leave
+  // the binade; that chunk is added site by site, and the next batch starts in the new binade
+  constexpr int WCB = 16;
+  while (i + WC <= end) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(s);
+    const int e = (int)((b >> 52) & 0x7FF) - 1023;
+    if (s < 0.0 && e >= emin && e < emin + ne) {
+      const int nb = min(WCB, (end - i) / WC);
+      const double2* tb = reinterpret_cast<const double2*>(tab) + (size_t)(i / WC) * ne + (e - emin);
+      double2 d[WCB];
+#pragma unroll
+      for (int k = 0; k < WCB; k++) d[k] = k < nb ? tb[(size_t)k * ne] : make_double2(0.0, 0.0);
+      const double sc = __longlong_as_double((long long)(1023 + 52 - e) << 52);  // 2^(52 - e)
+      const double isc = __longlong_as_double((long long)(1023 - 52 + e) << 52);  // 2^(e - 52)
+      bool go = true;
+      int q = 0;
+#pragma unroll
+      for (int k = 0; k < WCB; k++) {
+        if (go && k < nb) {
+          const double m = s * sc;  // an integer, |m| in [2^52, 2^53): its last mantissa bit is its parity
+          const double mn = m + ((__double_as_longlong(m) & 1) ? d[k].y : d[k].x);
+          if (mn > -9007199254740992.0) { s = mn * isc; q = k + 1; }  // still in the binade (NaN fails)
+          else go = false;
+        }
+      }
+      i += q * WC;
+      if (q == nb) continue;
+    }
+    elems(i, WC);  // leaves the binade, a positive or non-finite value, or below emin
+    i += WC;
+  }
+  elems(i, end - i);
+  out[ws] = s;
+}
+
 // one trial's rows into the (position, row) array: pr[phys(i)].y = row[i] + 1 (device row), read
 // straight from the pinned host staging (no copy-engine transfer, which would order this
 // stream's work behind other streams' copies); block 0 also takes the whole-chromosome null
@@ -1614,6 +1738,10 @@ struct Slot {
   hipEvent_t wev0 = nullptr, wev1 = nullptr;  // bracket the slot's last window null-sum launch
   bool wpend = false;             // its time not yet added to window_ms (read without blocking later)
   int users = 0;                  // batches submitted on this slot and not yet waited for
+  double* d_ctab = nullptr;       // chunk_table_kernel's table for the slot's rows (window_chunk_kernel)
+  size_t ctab_cap = 0;            // doubles
+  bool ctab_valid = false;        // built for the slot's rows with (ctab_emin, ctab_ne)
+  int ctab_emin = 0, ctab_ne = 0;
 };
 
 // one search_maxpos launch group (fsclg_search_submit / fsclg_search_wait): its stream,
@@ -1673,6 +1801,8 @@ struct fsclg_ctx {
   int32_t* d_chr_n = nullptr;
   int2* d_wtasks = nullptr;
   int n_wtasks = 0, wtask_cap = 0, wtask_er = -1;
+  int wtask_chunk = -1;                 // the dense task list is for window_chunk_kernel (256 per task) or not
+  std::vector<double> h_nullrows;       // the uploaded null rows (chunk_params)
   double window_ms = 0.0;
   int n_chr = 0;
   std::vector<int> h_chr_n;
@@ -1815,7 +1945,7 @@ int fsclg_close(fsclg_ctx* c) {
                   c->d_stats, c->d_dfail};
   for (void* p : ptrs) if (p) hipFree(p);
   for (Slot& S : c->slot) {
-    for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null}) if (p) hipFree(p);
+    for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null, (void*)S.d_ctab}) if (p) hipFree(p);
     for (void* p : {(void*)S.h_rows, (void*)S.h_null, (void*)S.p_wtasks}) if (p) hipHostFree(p);
     hipEventDestroy(S.ready);
     if (S.wev0) hipEventDestroy(S.wev0);
@@ -1878,6 +2008,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   std::vector<double> nul(1, 0.0);
   nul.insert(nul.end(), nullrow, nullrow + n_rows);
   if ((r = upload(&c->d_null, nul.data(), nul.size(), c->ustream))) return r;
+  c->h_nullrows = nul;
   std::vector<double> thr((size_t)n_iv + 1, 0.0);
   for (int j = 1; j < n_iv; j++) thr[j] = interval_threshold(j, log_ad_step);
   thr[0] = -__builtin_inf();     // iv 0 never steps down
@@ -1885,7 +2016,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->ustream))) return r;
   c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
   c->plan_dirty = true;
-  for (Slot& S : c->slot) S.win_valid = false;
+  for (Slot& S : c->slot) { S.win_valid = false; S.ctab_valid = false; }
   return FSCLG_OK;
 }
 
@@ -1908,7 +2039,7 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
     if ((r = upload(&S.d_pr, pr.data(), pr.size(), c->ustream))) return r;
     if ((r = upload<double>(&S.d_chr_null, nullptr, (size_t)n_chr, c->ustream))) return r;
     if ((r = upload<double>(&S.d_win_null, nullptr, (size_t)n_snps, c->ustream))) return r;
-    S.win_valid = false; S.win_er = -1;
+    S.win_valid = false; S.win_er = -1; S.ctab_valid = false;
     HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   }
   c->n_snps = n_snps;
@@ -1984,7 +2115,7 @@ int fsclg_slot_set_rows(fsclg_ctx* c, int slot, const uint32_t* row, const doubl
   int r;
   if ((r = ensure_row_staging(c, S))) return r;
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read the staging
-  S.win_valid = false;
+  S.win_valid = false; S.ctab_valid = false;
   if (row) {
     uint32_t mx = 0;
     for (int i = 0; i < c->n_snps; i++) mx = row[i] > mx ? row[i] : mx;  // vectorised validation
@@ -2033,7 +2164,7 @@ int fsclg_slot_set_rows_host(fsclg_ctx* c, int slot, const uint32_t* row, const 
   int r;
   if ((r = ensure_null_staging(c, S))) return r;
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read h_null
-  S.win_valid = false;
+  S.win_valid = false; S.ctab_valid = false;
   if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
   // read straight from the caller's portable pinned rows (one buffer can feed every device)
   hipLaunchKernelGGL(scatter_rows_kernel, dim3((c->n_snps + 1023) / 1024), dim3(256), 0, c->ustream, S.d_pr, row,
@@ -2144,6 +2275,42 @@ static int window_time(fsclg_ctx* c, Slot& S) {
 static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out);
 static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vector<int2>& todo);
 
+// window_chunk_kernel's parameters for windows of W sites: emin, the least binade in which a chunk
+// of 64 values cannot move the running integer m by 2^52 or more (2^emin >= 64 max |null|), and
+// ne binades up to the largest a window's sum can reach (|sum| <= W max |null|); false: use the
+// sequential kernel (too many rows for its LDS copy, or no finite null value)
+static bool chunk_params(fsclg_ctx* c, long long W, int& emin, int& ne) {
+  if (c->n_rows + 1 > WC_MAXROWS) return false;
+  double mx = 0.0;
+  for (double v : c->h_nullrows) if (std::isfinite(v)) mx = std::max(mx, std::fabs(v));
+  if (!(mx > 0.0)) return false;
+  int e1 = 0, e2 = 0;
+  std::frexp(64.0 * mx, &e1);            // 64 mx < 2^e1
+  std::frexp((double)W * mx, &e2);       // W mx < 2^e2: the largest binade is e2 - 1
+  emin = e1;
+  ne = std::max(1, e2 - e1 + 1);
+  return emin + ne - 1 <= 52;
+}
+
+// the slot's chunk table (after its rows' upload, on the upload stream)
+static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne) {
+  if (S.ctab_valid && S.ctab_emin == emin && S.ctab_ne == ne) return FSCLG_OK;
+  const int nch = (c->n_snps + WC - 1) / WC;
+  const size_t need = (size_t)nch * ne * 2;
+  if (S.ctab_cap < need) {
+    if (S.d_ctab) hipFree(S.d_ctab);
+    S.d_ctab = nullptr; S.ctab_cap = 0;
+    HIPCHK(hipMalloc((void**)&S.d_ctab, sizeof(double) * need), "hipMalloc chunk table");
+    S.ctab_cap = need;
+  }
+  const int nthr = nch * ne;
+  hipLaunchKernelGGL(chunk_table_kernel, dim3((nthr + 255) / 256), dim3(256), 0, c->ustream, S.d_pr, c->d_null,
+                     c->n_snps, emin, ne, S.d_ctab);
+  HIPCHK(hipGetLastError(), "launch chunk_table_kernel");
+  S.ctab_valid = true; S.ctab_emin = emin; S.ctab_ne = ne;
+  return FSCLG_OK;
+}
+
 static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* cells, int n_cells) {
   const long long W = 2ll * er + 1;
   Slot& S = c->slot[slot];
@@ -2164,14 +2331,21 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
     return launch_partial_windows(c, S, er, todo);
   }
   if (S.win_valid && S.win_er == er) return FSCLG_OK;
-  if (c->wtask_er != er) {
+  // every window start: the sequential kernel (its FP64 adds use issue slots the search kernels
+  // leave idle; the chunked kernel's loads compete with theirs for the texture path, measured
+  // slower overall) unless FSCLG_WINDOW_CHUNK=2
+  const int chunk_mode = getenv("FSCLG_WINDOW_CHUNK") ? atoi(getenv("FSCLG_WINDOW_CHUNK")) : 1;
+  int emin = 0, ne = 0;
+  const bool chunked = chunk_mode >= 2 && chunk_params(c, W, emin, ne);
+  const int per_task = chunked ? WN_WG : WN_WG * WN_PER;
+  if (c->wtask_er != er || c->wtask_chunk != (int)chunked) {
     std::vector<int2> tasks;
     for (int ch = 0; ch < c->n_chr; ch++) {
       const long long n = c->h_chr_n[ch];
       if (n <= W) continue;
       const int cnt = (int)(n - W + 1);  // window starts cs .. ce - 2er
-      for (int o = 0; o < cnt; o += WN_WG * WN_PER)
-        tasks.push_back(make_int2(c->h_chr_start[ch] + o, std::min(WN_WG * WN_PER, cnt - o)));
+      for (int o = 0; o < cnt; o += per_task)
+        tasks.push_back(make_int2(c->h_chr_start[ch] + o, std::min(per_task, cnt - o)));
     }
     // every launch reading the task list has completed (no batch runs on a slot being set up;
     // the other slot's window launch ran on this same stream)
@@ -2188,13 +2362,20 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
              "copy window tasks");
     HIPCHK(hipStreamSynchronize(c->ustream), "hipStreamSynchronize");
     c->wtask_er = er;
+    c->wtask_chunk = (int)chunked;
   }
   if (c->n_wtasks) {
     int r;
     if ((r = window_time(c, S))) return r;  // the slot's previous launch (long finished)
     HIPCHK(hipEventRecord(S.wev0, c->ustream), "hipEventRecord");
-    hipLaunchKernelGGL((window_null_kernel<WN_PER>), dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
-                       c->d_wtasks, (int)W, S.d_win_null);
+    if (chunked) {
+      if ((r = ensure_ctab(c, S, emin, ne))) return r;
+      hipLaunchKernelGGL(window_chunk_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
+                         c->n_rows + 1, c->d_wtasks, (int)W, emin, ne, S.d_ctab, S.d_win_null);
+    } else {
+      hipLaunchKernelGGL((window_null_kernel<WN_PER>), dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr,
+                         c->d_null, c->d_wtasks, (int)W, S.d_win_null);
+    }
     HIPCHK(hipGetLastError(), "launch window_null_kernel");
     HIPCHK(hipEventRecord(S.wev1, c->ustream), "hipEventRecord");
     HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");  // the slot's batches wait for it on the GPU
@@ -2260,8 +2441,18 @@ static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vect
   int r;
   if ((r = window_time(c, S))) return r;
   HIPCHK(hipEventRecord(S.wev0, c->ustream), "hipEventRecord");
-  hipLaunchKernelGGL((window_null_kernel<1>), dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
-                     (int)(2ll * er + 1), S.d_win_null);
+  // the active cells' windows of one trial (the pruned tail, where each trial waits for them):
+  // the chunked kernel, whose chain per window is ~50x shorter (FSCLG_WINDOW_CHUNK=0: sequential)
+  const int chunk_mode = getenv("FSCLG_WINDOW_CHUNK") ? atoi(getenv("FSCLG_WINDOW_CHUNK")) : 1;
+  int emin = 0, ne = 0;
+  if (chunk_mode >= 1 && chunk_params(c, 2ll * er + 1, emin, ne)) {
+    if ((r = ensure_ctab(c, S, emin, ne))) return r;
+    hipLaunchKernelGGL(window_chunk_kernel, dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, c->n_rows + 1,
+                       S.p_wtasks, (int)(2ll * er + 1), emin, ne, S.d_ctab, S.d_win_null);
+  } else {
+    hipLaunchKernelGGL((window_null_kernel<1>), dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
+                       (int)(2ll * er + 1), S.d_win_null);
+  }
   HIPCHK(hipGetLastError(), "launch window_null_kernel");
   HIPCHK(hipEventRecord(S.wev1, c->ustream), "hipEventRecord");
   HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");  // the slot's batches wait for it on the GPU

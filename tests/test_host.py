@@ -279,3 +279,76 @@ def test_interval_thresholds_reproduce_the_division(built, n_iv):
     down = ~up & (iv > 0) & (xs < T[iv])
     got = iv + up - down
     assert np.array_equal(got, ref)
+
+
+def _chunked_window_sum(v, W, a, emin, ne, C=64):
+    """Python restatement of window_chunk_kernel / chunk_table_kernel (fsclg.hip): the exact
+    chunked form of acc = 0.0; acc += v[i] for i = a .. a + W - 1."""
+    import math
+
+    def table(c, e):
+        vals = v[c * C:(c + 1) * C]
+        if len(vals) < C or any(not (x <= 0.0) or x == -math.inf for x in vals):
+            return None
+        u = math.ldexp(1.0, e - 52)
+        out = []
+        for p in (0, 1):
+            d, par = 0, p
+            for x in vals:
+                q = x / u
+                F = math.floor(q)
+                if q - F == 0.5:
+                    d += F + ((par + F) & 1)
+                    par = 0
+                else:
+                    R = round(q)
+                    d += R
+                    par = (par + R) & 1
+            out.append(d)
+        return out
+
+    s, i, end = 0.0, a, a + W
+    while i < end:  # head
+        if i % C == 0 and s <= -math.ldexp(1.0, emin):
+            break
+        s = s + v[i]
+        i += 1
+    while i + C <= end:  # chunks
+        e = math.frexp(-s)[1] - 1 if s < 0.0 else None
+        t = table(i // C, e) if e is not None and emin <= e < emin + ne else None
+        if t is not None:
+            u = math.ldexp(1.0, e - 52)
+            m = int(s / u)
+            mn = m + t[m & 1]
+            if mn > -(1 << 53):
+                s, i = mn * u, i + C
+                continue
+        for j in range(C):
+            s = s + v[i + j]
+        i += C
+    while i < end:
+        s = s + v[i]
+        i += 1
+    return s
+
+
+def test_chunked_window_sums_are_the_sequential_sums():
+    """The chunked window null sums (fsclg.hip window_chunk_kernel) restated in
+    Python: bit-identical to the sequential sum for windows at every offset, over null values
+    with short mantissas (ties at many binades), zeros and a positive value (its chunks fall back
+    to site-by-site adds)."""
+    import math
+    import random
+    rng = random.Random(11)
+    classes = [-rng.randint(1, 4000) / 64.0 if k % 3 == 0 else -rng.uniform(0.5, 60.0) for k in range(300)]
+    classes[5], classes[6] = 0.0, 3.5
+    v = [classes[rng.randrange(len(classes))] for _ in range(5000)]
+    mx = max(abs(x) for x in v)
+    W = 1800
+    emin = math.frexp(64 * mx)[1]
+    ne = math.frexp(W * mx)[1] - emin + 1
+    for a in list(range(0, 64)) + list(range(64, len(v) - W + 1, 53)):
+        seq = 0.0
+        for i in range(a, a + W):
+            seq = seq + v[i]
+        assert _chunked_window_sum(v, W, a, emin, ne).hex() == seq.hex(), a
