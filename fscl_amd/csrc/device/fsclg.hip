@@ -1493,7 +1493,6 @@ search_maxpos_split_kernel(Params P) {
 // read once from LDS feeds all of them, each accumulator in its own ascending order); the
 // block stages the elements its 1024 windows span through an LDS tile.
 constexpr int WN_WG = 256, WN_PER = 4, WN_TILE = 4096;
-constexpr int WC_MAXROWS = 4096;  // window_chunk_kernel's LDS copy of the null rows (larger tables: the sequential kernel)
 
 // A block's staging of a tile is one round of independent row loads (all of a full tile's rows
 // before any null value), and its sums read the tile eight elements at a time before adding
@@ -1578,23 +1577,23 @@ window_null_kernel(const uint2* __restrict__ pr, const double* __restrict__ null
 // binade, one holding a positive or non-finite value (NaN in the table), the windows' ends and
 // the first sites (until |S| >= 2^emin, where a binade spans at least a chunk) are added site by
 // site in order.  Same result as the sequential chain, bit for bit, for every window.
-constexpr int WC = 64;  // chunk length, aligned to the site index
+constexpr int WC = 64;   // chunk length, aligned to the site index
+constexpr int WCG = 16;  // chunks per wave-uniform group (their table entries: one scalar load run)
 
-// chunk c, binade e = emin + k: tab[(c ne + k) 2 + p] = the integer increment of m over the
-// chunk's 64 sequential adds for an even (p = 0) or odd (p = 1) m on entry, as an exact double
-// (|increment| < 2^52 by the choice of emin); NaN when the chunk holds a value that is positive,
-// not finite, or lies past the last site
+// binade e = emin + k, chunk c: tab[k * nstride + c] = (d0, d1 - d0), d0 / d1 the increment of the
+// chunk's 64 sequential adds for an even / odd m on entry, exact doubles (|increment| < 2^52 by the
+// choice of emin), so that the increment is fma(parity, d1 - d0, d0), exactly; NaN when the chunk holds a value that is positive, not finite, or lies past the last
+// site.  Binade-major, so that a group of consecutive chunks at one binade is one contiguous run;
+// nstride = chunks + WCG (the padding entries are NaN).
 __global__ void __launch_bounds__(256) chunk_table_kernel(const uint2* __restrict__ pr,
                                                           const double* __restrict__ nullrow, int n_snps, int emin,
-                                                          int ne, double* __restrict__ tab) {
+                                                          int ne, int nstride, double2* __restrict__ tab) {
   const int t = blockIdx.x * 256 + threadIdx.x;
-  const int nch = (n_snps + WC - 1) / WC;
-  if (t >= nch * ne) return;
-  const int c = t / ne, k = t - c * ne;
+  if (t >= nstride * ne) return;
+  const int k = t / nstride, c = t - k * nstride;
   const int e = emin + k;
-  double* o = tab + ((size_t)c * ne + k) * 2;
   const double nan = __longlong_as_double(0x7FF8000000000000ll);
-  if ((c + 1) * WC > n_snps) { o[0] = nan; o[1] = nan; return; }
+  if ((c + 1) * WC > n_snps) { tab[t] = make_double2(nan, nan); return; }
   const double sc = __longlong_as_double((long long)(1023 + 52 - e) << 52);  // 2^(52 - e), e <= 52
   long long d0 = 0, d1 = 0;
   int p0 = 0, p1 = 1;
@@ -1614,77 +1613,97 @@ __global__ void __launch_bounds__(256) chunk_table_kernel(const uint2* __restric
       d1 += R; p1 = (int)((p1 + R) & 1);
     }
   }
-  o[0] = ok ? (double)d0 : nan;
-  o[1] = ok ? (double)d1 : nan;
+  tab[t] = ok ? make_double2((double)d0, (double)(d1 - d0)) : make_double2(nan, nan);
 }
 
-// one window per thread, 256 consecutive window starts per block (tasks: [start, count])
+// A wave sums the windows of 64 consecutive starts (one per lane; 256 per block, tasks: [start,
+// count]), walking the absolute chunks in order, every lane at the same chunk:
+//  * interior groups: while every lane is at a whole chunk of its window, at least 2^emin in
+//    magnitude and in one binade e, WCG chunks' entries for e are read by the whole wave at once
+//    (uniform address: scalar loads), and each chunk is one add per lane on the integer m; a chunk
+//    that some lane would leave the binade with (or a NaN entry) ends the group and goes to
+//  * the general step: each lane takes its chunk from the table when it can (its own entry), or
+//    adds the chunk's sites of its window in order, the chunk's null values loaded by the wave
+//    (one site per lane) and broadcast lane by lane.
+// The windows' ends, the first sites (until |S| >= 2^emin) and the binade crossings take the
+// general step; lanes' sums differ by their first few sites only, so they cross together.
 __global__ void __launch_bounds__(WN_WG)
-window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nullrow, int n_rows1,
-                    const int2* __restrict__ tasks, int W, int emin, int ne, const double* __restrict__ tab,
-                    double* __restrict__ out) {
-  __shared__ double nul[WC_MAXROWS];
+window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nullrow,
+                    const int2* __restrict__ tasks, int W, int emin, int ne, int nstride,
+                    const double2* __restrict__ tab, double* __restrict__ out) {
   __builtin_amdgcn_s_setprio(2);  // beside the search kernels' waves, which wait on memory
-  for (int r = threadIdx.x; r < n_rows1; r += WN_WG) nul[r] = nullrow[r];
-  __syncthreads();
   const int2 t = tasks[blockIdx.x];
-  if ((int)threadIdx.x >= t.y) return;
-  const int ws = t.x + (int)threadIdx.x, end = ws + W;
+  const int lane = threadIdx.x & 63;
+  const int w0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));  // the wave's first window in the block
+  if (w0 >= t.y) return;
+  const int nv = min(64, t.y - w0);
+  const bool valid = lane < nv;
+  const int ws0 = t.x + w0, wsL = ws0 + nv - 1;
+  const int ws = ws0 + min(lane, nv - 1), end = ws + W;  // invalid lanes shadow the last valid one
   double s = 0.0;
-  // sites [i, i + n) added in order, their rows loaded eight at a time
-  auto elems = [&](int i, int n) {
-    for (int b = 0; b < n; b += 8) {
-      uint32_t rr[8];
+  const int cend = ((wsL + W - 1) >> 6) + 1;
+  const int fast_lo = (wsL + WC - 1) >> 6;  // chunks at or past every lane's start
+  const int fast_hi = (ws0 + W) >> 6;       // chunks ending at or before every lane's end
+  const double TWO53 = 9007199254740992.0;
+  int c = ws0 >> 6;
+  while (c < cend) {
+    if (c >= fast_lo && c < fast_hi) {  // uniform (c stays uniform: every branch that moves it is)
+      const int e = (int)((__double_as_longlong(s) >> 52) & 0x7FF) - 1023;
+      const int eu = __builtin_amdgcn_readfirstlane(e);
+      if (eu >= emin && eu < emin + ne && __builtin_amdgcn_ballot_w64(!(s < 0.0) || e != eu) == 0ull) {
+        const int gn = min(WCG, fast_hi - c);
+        // uniform address, read-only for the kernel's life: through the constant address space, so
+        // that the group's entries are scalar loads (registers shared by the wave; no texture path)
+        typedef const __attribute__((address_space(4))) double cdouble;
+        cdouble* tb = (cdouble*)(tab + (size_t)(eu - emin) * nstride + c);  // the padding covers c + WCG
+        double d0[WCG], dd[WCG];
 #pragma unroll
-      for (int q = 0; q < 8; q++) rr[q] = b + q < n ? pr[phys((uint32_t)(i + b + q))].y : 0u;
+        for (int k = 0; k < WCG; k++) { d0[k] = tb[2 * k]; dd[k] = tb[2 * k + 1]; }
+        const double sc = __longlong_as_double((long long)(1023 + 52 - eu) << 52);   // 2^(52 - e)
+        const double isc = __longlong_as_double((long long)(1023 - 52 + eu) << 52);  // 2^(e - 52)
+        double m = s * sc;  // an integer, |m| in [2^52, 2^53): its last mantissa bit is its parity
+        int j = gn;
+        bool run = true;
 #pragma unroll
-      for (int q = 0; q < 8; q++)
-        if (b + q < n) s += nul[rr[q]];
-    }
-  };
-  // head: site by site until |S| >= 2^emin at a chunk boundary
-  const double lim = -__longlong_as_double((long long)(1023 + emin) << 52);  // -2^emin
-  int i = ws;
-  while (i < end) {
-    const int n = min(WC - (i & (WC - 1)), end - i);  // to the next chunk boundary
-    if ((i & (WC - 1)) == 0 && s <= lim) break;
-    elems(i, n);
-    i += n;
-  }
-  // chunks, in batches of WCB: the batch's table entries for the running binade are loaded together
-  // (one load latency per batch, not per chunk), then applied in order until a chunk would leave
-  // the binade; that chunk is added site by site, and the next batch starts in the new binade
-  constexpr int WCB = 16;
-  while (i + WC <= end) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(s);
-    const int e = (int)((b >> 52) & 0x7FF) - 1023;
-    if (s < 0.0 && e >= emin && e < emin + ne) {
-      const int nb = min(WCB, (end - i) / WC);
-      const double2* tb = reinterpret_cast<const double2*>(tab) + (size_t)(i / WC) * ne + (e - emin);
-      double2 d[WCB];
-#pragma unroll
-      for (int k = 0; k < WCB; k++) d[k] = k < nb ? tb[(size_t)k * ne] : make_double2(0.0, 0.0);
-      const double sc = __longlong_as_double((long long)(1023 + 52 - e) << 52);  // 2^(52 - e)
-      const double isc = __longlong_as_double((long long)(1023 - 52 + e) << 52);  // 2^(e - 52)
-      bool go = true;
-      int q = 0;
-#pragma unroll
-      for (int k = 0; k < WCB; k++) {
-        if (go && k < nb) {
-          const double m = s * sc;  // an integer, |m| in [2^52, 2^53): its last mantissa bit is its parity
-          const double mn = m + ((__double_as_longlong(m) & 1) ? d[k].y : d[k].x);
-          if (mn > -9007199254740992.0) { s = mn * isc; q = k + 1; }  // still in the binade (NaN fails)
-          else go = false;
+        for (int k = 0; k < WCG; k++) {
+          if (run && k < gn) {  // uniform
+            const double mn = m + __builtin_fma((double)(__double2loint(m) & 1), dd[k], d0[k]);
+            if (__builtin_amdgcn_ballot_w64(!(mn > -TWO53))) { j = k; run = false; }  // leaves the binade, or NaN
+            else m = mn;
+          }
         }
+        s = m * isc;
+        c += j;
+        if (j == gn) continue;
       }
-      i += q * WC;
-      if (q == nb) continue;
     }
-    elems(i, WC);  // leaves the binade, a positive or non-finite value, or below emin
-    i += WC;
+    // the general step for chunk c
+    const int cb = c * WC;
+    const int lo = max(ws - cb, 0), hi = min(end - cb, WC);  // the lane's sites of the chunk: [lo, hi)
+    bool need = lo < hi;
+    if (need && lo == 0 && hi == WC && s < 0.0) {
+      const int e = (int)((__double_as_longlong(s) >> 52) & 0x7FF) - 1023;
+      if (e >= emin && e < emin + ne) {
+        const double2 d = tab[(size_t)(e - emin) * nstride + c];
+        const double sc = __longlong_as_double((long long)(1023 + 52 - e) << 52);
+        const double isc = __longlong_as_double((long long)(1023 - 52 + e) << 52);
+        const double m = s * sc;
+        const double mn = m + __builtin_fma((double)(__double2loint(m) & 1), d.y, d.x);
+        if (mn > -TWO53) { s = mn * isc; need = false; }
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(need)) {
+      const double v = nullrow[pr[phys((uint32_t)(cb + lane))].y];  // cb + 63 is inside the padded array
+      const int2 vv = make_int2(__double2loint(v), __double2hiint(v));
+#pragma unroll 8
+      for (int q = 0; q < WC; q++) {
+        const double x = __hiloint2double(__builtin_amdgcn_readlane(vv.y, q), __builtin_amdgcn_readlane(vv.x, q));
+        if (need && q >= lo && q < hi) s += x;
+      }
+    }
+    c++;
   }
-  elems(i, end - i);
-  out[ws] = s;
+  if (valid) out[ws] = s;
 }
 
 // one trial's rows into the (position, row) array: pr[phys(i)].y = row[i] + 1 (device row), read
@@ -1738,8 +1757,8 @@ struct Slot {
   hipEvent_t wev0 = nullptr, wev1 = nullptr;  // bracket the slot's last window null-sum launch
   bool wpend = false;             // its time not yet added to window_ms (read without blocking later)
   int users = 0;                  // batches submitted on this slot and not yet waited for
-  double* d_ctab = nullptr;       // chunk_table_kernel's table for the slot's rows (window_chunk_kernel)
-  size_t ctab_cap = 0;            // doubles
+  double2* d_ctab = nullptr;      // chunk_table_kernel's table for the slot's rows (window_chunk_kernel)
+  size_t ctab_cap = 0;            // entries
   bool ctab_valid = false;        // built for the slot's rows with (ctab_emin, ctab_ne)
   int ctab_emin = 0, ctab_ne = 0;
 };
@@ -2278,9 +2297,8 @@ static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vect
 // window_chunk_kernel's parameters for windows of W sites: emin, the least binade in which a chunk
 // of 64 values cannot move the running integer m by 2^52 or more (2^emin >= 64 max |null|), and
 // ne binades up to the largest a window's sum can reach (|sum| <= W max |null|); false: use the
-// sequential kernel (too many rows for its LDS copy, or no finite null value)
+// sequential kernel (no finite null value, or binades past the double's integer range)
 static bool chunk_params(fsclg_ctx* c, long long W, int& emin, int& ne) {
-  if (c->n_rows + 1 > WC_MAXROWS) return false;
   double mx = 0.0;
   for (double v : c->h_nullrows) if (std::isfinite(v)) mx = std::max(mx, std::fabs(v));
   if (!(mx > 0.0)) return false;
@@ -2292,20 +2310,23 @@ static bool chunk_params(fsclg_ctx* c, long long W, int& emin, int& ne) {
   return emin + ne - 1 <= 52;
 }
 
+// entries per binade of the chunk table: the chunks, then WCG padding entries for a group's reads
+static int ctab_stride(const fsclg_ctx* c) { return (c->n_snps + WC - 1) / WC + WCG; }
+
 // the slot's chunk table (after its rows' upload, on the upload stream)
 static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne) {
   if (S.ctab_valid && S.ctab_emin == emin && S.ctab_ne == ne) return FSCLG_OK;
-  const int nch = (c->n_snps + WC - 1) / WC;
-  const size_t need = (size_t)nch * ne * 2;
+  const int nstride = ctab_stride(c);
+  const size_t need = (size_t)nstride * ne;
   if (S.ctab_cap < need) {
     if (S.d_ctab) hipFree(S.d_ctab);
     S.d_ctab = nullptr; S.ctab_cap = 0;
-    HIPCHK(hipMalloc((void**)&S.d_ctab, sizeof(double) * need), "hipMalloc chunk table");
+    HIPCHK(hipMalloc((void**)&S.d_ctab, sizeof(double2) * need), "hipMalloc chunk table");
     S.ctab_cap = need;
   }
-  const int nthr = nch * ne;
-  hipLaunchKernelGGL(chunk_table_kernel, dim3((nthr + 255) / 256), dim3(256), 0, c->ustream, S.d_pr, c->d_null,
-                     c->n_snps, emin, ne, S.d_ctab);
+  const long long nthr = (long long)nstride * ne;
+  hipLaunchKernelGGL(chunk_table_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, c->ustream, S.d_pr,
+                     c->d_null, c->n_snps, emin, ne, nstride, S.d_ctab);
   HIPCHK(hipGetLastError(), "launch chunk_table_kernel");
   S.ctab_valid = true; S.ctab_emin = emin; S.ctab_ne = ne;
   return FSCLG_OK;
@@ -2331,10 +2352,9 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
     return launch_partial_windows(c, S, er, todo);
   }
   if (S.win_valid && S.win_er == er) return FSCLG_OK;
-  // every window start: the sequential kernel (its FP64 adds use issue slots the search kernels
-  // leave idle; the chunked kernel's loads compete with theirs for the texture path, measured
-  // slower overall) unless FSCLG_WINDOW_CHUNK=2
-  const int chunk_mode = getenv("FSCLG_WINDOW_CHUNK") ? atoi(getenv("FSCLG_WINDOW_CHUNK")) : 1;
+  // every window start: the chunked kernel (FSCLG_WINDOW_CHUNK=1: the sequential
+  // kernel here and the chunked one for partial sets, 0: sequential everywhere)
+  const int chunk_mode = getenv("FSCLG_WINDOW_CHUNK") ? atoi(getenv("FSCLG_WINDOW_CHUNK")) : 2;
   int emin = 0, ne = 0;
   const bool chunked = chunk_mode >= 2 && chunk_params(c, W, emin, ne);
   const int per_task = chunked ? WN_WG : WN_WG * WN_PER;
@@ -2371,7 +2391,7 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
     if (chunked) {
       if ((r = ensure_ctab(c, S, emin, ne))) return r;
       hipLaunchKernelGGL(window_chunk_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
-                         c->n_rows + 1, c->d_wtasks, (int)W, emin, ne, S.d_ctab, S.d_win_null);
+                         c->d_wtasks, (int)W, emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null);
     } else {
       hipLaunchKernelGGL((window_null_kernel<WN_PER>), dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr,
                          c->d_null, c->d_wtasks, (int)W, S.d_win_null);
@@ -2443,12 +2463,12 @@ static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vect
   HIPCHK(hipEventRecord(S.wev0, c->ustream), "hipEventRecord");
   // the active cells' windows of one trial (the pruned tail, where each trial waits for them):
   // the chunked kernel, whose chain per window is ~50x shorter (FSCLG_WINDOW_CHUNK=0: sequential)
-  const int chunk_mode = getenv("FSCLG_WINDOW_CHUNK") ? atoi(getenv("FSCLG_WINDOW_CHUNK")) : 1;
+  const int chunk_mode = getenv("FSCLG_WINDOW_CHUNK") ? atoi(getenv("FSCLG_WINDOW_CHUNK")) : 2;
   int emin = 0, ne = 0;
   if (chunk_mode >= 1 && chunk_params(c, 2ll * er + 1, emin, ne)) {
     if ((r = ensure_ctab(c, S, emin, ne))) return r;
-    hipLaunchKernelGGL(window_chunk_kernel, dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, c->n_rows + 1,
-                       S.p_wtasks, (int)(2ll * er + 1), emin, ne, S.d_ctab, S.d_win_null);
+    hipLaunchKernelGGL(window_chunk_kernel, dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
+                       (int)(2ll * er + 1), emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null);
   } else {
     hipLaunchKernelGGL((window_null_kernel<1>), dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
                        (int)(2ll * er + 1), S.d_win_null);

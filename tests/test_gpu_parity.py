@@ -330,24 +330,25 @@ def test_full_size_configs_match_oracle(built, tmp, name, gen, opts):
         assert fscl_amd.get_stats()["window_ms"] > 0
 
 
-@pytest.mark.parametrize("mode", ["0", "2"])
-def test_window_sum_kernels_match_oracle(built, tmp, monkeypatch, mode):
+@pytest.mark.parametrize("mode,er", [("0", 300), ("1", 300), ("2", 300), ("2", 3000)])
+def test_window_sum_kernels_match_oracle(built, tmp, monkeypatch, mode, er):
     """The window null sums (scan-chromosome.c:92-94) by each kernel for every trial:
-    FSCLG_WINDOW_CHUNK=0 the sequential chains for every window start, 2 the exact chunked sums
-     for every window start (by default the chunked kernel serves only the
-    pruned tail's few windows).  Windows of 2*300+1 sites on 2 chromosomes, with permutations:
-    bit-identical to the oracle."""
+    FSCLG_WINDOW_CHUNK=0 the sequential chains for every window start, 1 those for the dense
+    trials and the exact chunked sums for the pruned tail's few windows, 2 (the
+    default) the chunked sums for every window start.  Windows of 2*300+1 sites (a few chunks
+    each: mostly the general step) and 2*3000+1 (~94 chunks: wave-uniform groups) on 2
+    chromosomes, with permutations: bit-identical to the oracle."""
     monkeypatch.setenv("FSCLG_WINDOW_CHUNK", mode)
     snp = tmp / "win.snp"
     synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=8_000_000, snps_per_chr=8000, n=60, seed=93,
                                                   sweeps_per_chr=1))
-    opts = ["--coarse-grid-spacing=100000", "--n-permute=25", "--eval-range=300"]
+    opts = ["--coarse-grid-spacing=100000", "--n-permute=25", f"--eval-range={er}"]
     run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     kw = _kw([o for o in opts if not o.startswith("--eval-range=")])
-    kw["eval_range"] = 300
+    kw["eval_range"] = er
     fscl_amd.reset_stats()
     scan = fscl_amd.run(snp, tmp / "g.txt", **kw)
-    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), f"windows mode {mode}")
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), f"windows mode {mode} er {er}")
     assert fscl_amd.get_stats()["window_ms"] > 0
 
 

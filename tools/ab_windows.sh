@@ -5,7 +5,7 @@ OUT=gpurun_out/ab_windows
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 600 --timeout-method thread -k "C5 or windowed or window" > $OUT/parity.log 2>&1 || { tail -30 $OUT/parity.log; exit 1; }
 tail -1 $OUT/parity.log
-for r in 1 2; do
+for r in $(seq ${AB_ROUNDS:-2}); do
   for v in chunk seq chunk2; do
     E=""; [ $v = seq ] && E="FSCLG_WINDOW_CHUNK=0"; [ $v = chunk2 ] && E="FSCLG_WINDOW_CHUNK=2"
     env $E timeout -k 10 600 python bench.py --config C5 --chromosomes 4 --n-permute 300 --steps 1 --warmup 0 --no-cpu-baseline > $OUT/c5_${v}_$r.json 2> $OUT/c5_${v}_$r.err || exit 1
