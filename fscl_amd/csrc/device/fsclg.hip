@@ -2922,8 +2922,9 @@ int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
       }
       memset(B.p_ctrace + 8 * (size_t)B.trace_n, 0, sizeof(unsigned long long) * 16008);
     }
-    if (FILE* f = fopen(getenv("FSCLG_CELL_TRACE"), "ab")) {
-      const unsigned long long nn = (unsigned long long)nu;
+    if (FILE* f = fopen(getenv("FSCLG_CELL_TRACE"), "ab")) {  // header: n | batch << 40 | split << 48
+      const unsigned long long nn = (unsigned long long)nu | ((unsigned long long)batch << 40) |
+                                    ((unsigned long long)B.split << 48);
       fwrite(&nn, sizeof nn, 1, f);
       fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
       fclose(f);

@@ -9,7 +9,7 @@ import numpy as np
 raw = np.fromfile(sys.argv[1], dtype=np.uint64)
 i, k = 0, 0
 while i < raw.size:
-    n = int(raw[i]); i += 1
+    n = int(raw[i]) & 0xFFFFFFFFFF; i += 1  # header: n | batch << 40 | split << 48
     a = raw[i:i + 8 * n].reshape(n, 8).astype(np.int64); i += 8 * n
     a = a[a[:, 0] > 0]  # idle blocks of the XCD placement
     n = len(a)
