@@ -101,7 +101,7 @@ EXPORTS = [
     "fscl_amd_get_stats", "fscl_amd_reset_stats", "fscl_amd_shutdown", "fscl_amd_partition",
     "fscl_amd_set_devices", "fscl_amd_n_devices", "fscl_amd_set_ranks_shm", "fscl_amd_srand",
     "fscl_amd_set_dump_output", "fsclg_host_alloc", "fsclg_host_free", "fsclg_slot_wait",
-    "fsclg_slot_set_rows_host",
+    "fsclg_slot_set_rows_host", "fsclg_slot_set_rows_packed",
     "fsclg_open", "fsclg_close", "fsclg_last_error", "fsclg_device_count", "fsclg_upload_tables",
     "fsclg_upload_snps", "fsclg_set_rows", "fsclg_set_chr_null", "fsclg_set_alpha_grid", "fsclg_search_maxpos",
     "fsclg_search_points", "fsclg_get_stats", "fsclg_reset_stats", "fsclg_interval_thresholds",

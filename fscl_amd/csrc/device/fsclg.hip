@@ -1709,27 +1709,39 @@ window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nul
 // one trial's rows into the (position, row) array: pr[phys(i)].y = row[i] + 1 (device row), read
 // straight from the pinned host staging (no copy-engine transfer, which would order this
 // stream's work behind other streams' copies); block 0 also takes the whole-chromosome null
-// sums.  row == null: the uploaded rows (pr0).
-__global__ void __launch_bounds__(256) scatter_rows_kernel(uint2* __restrict__ pr, const uint32_t* __restrict__ row,
+// sums.  row == null: the uploaded rows (pr0).  T: the staging's row width (1, 2 or 4 bytes:
+// the narrowest that holds the table's rows, so that the PCIe reads are as few as can be).
+template <typename T>
+__global__ void __launch_bounds__(256) scatter_rows_kernel(uint2* __restrict__ pr, const T* __restrict__ row,
                                                            const uint2* __restrict__ pr0, int n,
                                                            double* __restrict__ chr_null,
                                                            const double* __restrict__ chr_null_src, int n_chr) {
-  // four sites per thread: one 16-B read of the pinned host rows (PCIe reads are few and
-  // wide rather than one per site; the staging is page-aligned)
-  const int i = 4 * (blockIdx.x * 256 + threadIdx.x);
-  if (i + 3 < n) {
-    if (row) {
-      const uint4 r4 = *reinterpret_cast<const uint4*>(row + i);
-      pr[phys(i)].y = r4.x + 1u; pr[phys(i + 1)].y = r4.y + 1u; pr[phys(i + 2)].y = r4.z + 1u;
-      pr[phys(i + 3)].y = r4.w + 1u;
-    } else {
-      for (int k = 0; k < 4; k++) pr[phys(i + k)].y = pr0[phys(i + k)].y;
+  // a block takes 256 * E sites: one 16-B read of the pinned host rows per thread (PCIe reads
+  // few and wide; the staging is page-aligned) into an LDS tile, then each thread stores sites
+  // t, t + 256, ..., so that a wave's stores cover consecutive sites
+  constexpr int E = 16 / sizeof(T);
+  __shared__ __attribute__((aligned(16))) T tile[256 * E];
+  const int t = threadIdx.x, base = blockIdx.x * 256 * E;
+  if (row) {
+    const int i = base + E * t;
+    if (i + E <= n) *reinterpret_cast<uint4*>(&tile[E * t]) = *reinterpret_cast<const uint4*>(row + i);
+    else
+      for (int k = 0; k < E; k++) if (i + k < n) tile[E * t + k] = row[i + k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      const int q = base + 256 * k + t;
+      if (q < n) pr[phys(q)].y = (uint32_t)tile[256 * k + t] + 1u;
     }
   } else {
-    for (int k = i; k < n; k++) pr[phys(k)].y = row ? row[k] + 1u : pr0[phys(k)].y;
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      const int q = base + 256 * k + t;
+      if (q < n) pr[phys(q)].y = pr0[phys(q)].y;
+    }
   }
   if (blockIdx.x == 0 && chr_null_src)
-    for (int c = threadIdx.x; c < n_chr; c += 256) chr_null[c] = chr_null_src[c];
+    for (int c = t; c < n_chr; c += 256) chr_null[c] = chr_null_src[c];
 }
 
 }  // namespace
@@ -2142,9 +2154,9 @@ int fsclg_slot_set_rows(fsclg_ctx* c, int slot, const uint32_t* row, const doubl
     if (row != S.h_rows) memcpy(S.h_rows, row, sizeof(uint32_t) * c->n_snps);
   }
   if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3((c->n_snps + 1023) / 1024), dim3(256), 0, c->ustream, S.d_pr,
-                     row ? S.h_rows : nullptr, c->d_pr0, c->n_snps, S.d_chr_null, chr_null ? S.h_null : nullptr,
-                     c->n_chr);
+  hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, dim3((c->n_snps + 1023) / 1024), dim3(256), 0, c->ustream,
+                     S.d_pr, row ? S.h_rows : nullptr, c->d_pr0, c->n_snps, S.d_chr_null,
+                     chr_null ? S.h_null : nullptr, c->n_chr);
   HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
   HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   return FSCLG_OK;
@@ -2174,8 +2186,14 @@ int fsclg_slot_wait(fsclg_ctx* c, int slot) {
 }
 
 int fsclg_slot_set_rows_host(fsclg_ctx* c, int slot, const uint32_t* row, const double* chr_null) {
+  return fsclg_slot_set_rows_packed(c, slot, row, 4, chr_null);
+}
+
+int fsclg_slot_set_rows_packed(fsclg_ctx* c, int slot, const void* row, int row_bytes, const double* chr_null) {
   if (!c || !c->d_pr0) return set_err(FSCLG_E_STATE, "snps not uploaded");
   if (!row) return set_err(FSCLG_E_ARG, "rows");
+  if (!(row_bytes == 4 || (row_bytes == 2 && c->n_rows <= 0x10000) || (row_bytes == 1 && c->n_rows <= 0x100)))
+    return set_err(FSCLG_E_ARG, "row width");
   if (slot < 0 || slot >= NSLOT) return set_err(FSCLG_E_ARG, "slot");
   Slot& S = c->slot[slot];
   if (S.users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
@@ -2186,8 +2204,18 @@ int fsclg_slot_set_rows_host(fsclg_ctx* c, int slot, const uint32_t* row, const 
   S.win_valid = false; S.ctab_valid = false;
   if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
   // read straight from the caller's portable pinned rows (one buffer can feed every device)
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3((c->n_snps + 1023) / 1024), dim3(256), 0, c->ustream, S.d_pr, row,
-                     c->d_pr0, c->n_snps, S.d_chr_null, chr_null ? S.h_null : nullptr, c->n_chr);
+  const double* cn = chr_null ? S.h_null : nullptr;
+  const int per = 256 * (16 / row_bytes);  // sites per block
+  const dim3 grid((c->n_snps + per - 1) / per);
+  if (row_bytes == 1)
+    hipLaunchKernelGGL(scatter_rows_kernel<uint8_t>, grid, dim3(256), 0, c->ustream, S.d_pr,
+                       static_cast<const uint8_t*>(row), c->d_pr0, c->n_snps, S.d_chr_null, cn, c->n_chr);
+  else if (row_bytes == 2)
+    hipLaunchKernelGGL(scatter_rows_kernel<uint16_t>, grid, dim3(256), 0, c->ustream, S.d_pr,
+                       static_cast<const uint16_t*>(row), c->d_pr0, c->n_snps, S.d_chr_null, cn, c->n_chr);
+  else
+    hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, grid, dim3(256), 0, c->ustream, S.d_pr,
+                       static_cast<const uint32_t*>(row), c->d_pr0, c->n_snps, S.d_chr_null, cn, c->n_chr);
   HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
   HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   return FSCLG_OK;
@@ -2203,8 +2231,8 @@ int fsclg_set_chr_null(fsclg_ctx* c, const double* chr_null) {
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");
   memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
   // the null sums only: a one-block scatter over no sites
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3(1), dim3(256), 0, c->ustream, S.d_pr, nullptr, c->d_pr0, 0,
-                     S.d_chr_null, S.h_null, c->n_chr);
+  hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, dim3(1), dim3(256), 0, c->ustream, S.d_pr, nullptr, c->d_pr0,
+                     0, S.d_chr_null, S.h_null, c->n_chr);
   HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
   HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   return FSCLG_OK;

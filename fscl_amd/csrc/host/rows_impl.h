@@ -1,0 +1,121 @@
+/* The row-array routines of the permutation trials, for one staging width: included by scan.c
+   once per width with ROW_T (uint8_t, uint16_t or uint32_t) and ROW_SFX defined.  The trials'
+   rows are staged at the narrowest width that holds the device table's rows (D.rb bytes), so
+   that a candidate permutation moves fewer bytes on the host and every device's upload reads
+   fewer over PCIe; the values, and so every result, are the same at any width. */
+#define ROW_CAT2(a, b) a##_##b
+#define ROW_CAT(a, b) ROW_CAT2(a, b)
+
+/* init_scan_result's window sum (scan-chromosome.c:92-94): sequential from 0.0 over the
+   whole chromosome for the given rows */
+static void ROW_CAT(chr_null_sums, ROW_SFX)(const ROW_T *row, double *out) {
+  int c, i;
+#pragma omp parallel for schedule(dynamic, 1) private(i) if (D.n_chr > 1)
+  for (c = 0; c < D.n_chr; c++) {
+    double acc = 0.;
+    for (i = D.chr_start[c]; i < D.chr_start[c] + D.chr_n[c]; i++) acc += D.nullrow[row[i]];
+    out[c] = acc;
+  }
+}
+
+/* scan-chromosome.c:336-389 on the row array: blocks of consecutive sites (length ~ 1 +
+   Exp(nbp), extended to at least scan_width_mb on the same chromosome) are swapped into place;
+   positions never move.  Q9: a block running past the end is shifted left (j -= k - n) instead
+   of indexing p[-m] as the reference does; such events are counted. */
+static int ROW_CAT(block_permute, ROW_SFX)(ROW_T *prow, const ROW_T *row, const snp_t *snps, int n, double nbp,
+                                           double width_mb, fh_rand_t *g, unsigned long long *negj,
+                                           const volatile unsigned *gen, unsigned my_gen) {
+  int i = 0, j, k;
+  const double width = width_mb * 1e6;
+  const int piece = (1 << 20) / (int)sizeof(ROW_T);
+  for (i = 0; i < n; i += piece) { /* in 1 MB pieces: a cancelled candidate stops soon */
+    if (gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1;
+    memcpy(prow + i, row + i, sizeof(ROW_T) * (size_t)(n - i < piece ? n - i : piece));
+  }
+  i = 0;
+  while (i < n) {
+    const int r1 = fh_rand(g), r2 = fh_rand(g);
+    if (gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1; /* speculation cancelled */
+    j = r1 / (2147483647 + 1.0) * n;
+    if (r2 == 0) k = n; /* Q10: log(0) */
+    else k = j + (int)(-1.0 / nbp * log(r2 / (2147483647 + 1.0)));
+    /* scan-chromosome.c:355-357: extend k while on j's chromosome and within width of
+       pos[j]; positions ascend within a chromosome, so the stop is a lower bound */
+    if (k >= 0 && k < n && snps[k].chr == snps[j].chr) {
+      const int c = snps[j].chr, ce = D.chr_start[c] + D.chr_n[c];
+      const int32_t pj = D.pos[j];
+      int lo = k, hi = ce, step = 1; /* first index in [k, ce) with pos - pj >= width, else ce */
+      while (lo + step < ce && (double)(D.pos[lo + step] - pj) < width) { lo += step; step <<= 1; } /* gallop */
+      if (lo + step < ce) hi = lo + step;
+      if ((double)(D.pos[lo] - pj) < width) lo++; /* lo itself is inside (or is k, unchecked) */
+      while (lo < hi) {
+        const int m = lo + (hi - lo) / 2;
+        if ((double)(D.pos[m] - pj) < width) lo = m + 1; else hi = m;
+      }
+      k = lo;
+    }
+    if (i + (k - j) >= n) k = n;
+    if (k > n) { (*negj)++; j -= k - n; k = n; }
+    {
+      /* scan-chromosome.c:365-372: swap p[i++] with p[j++] while j < k and i < n; disjoint
+         ranges in one vectorisable pass, overlapping ones element by element as written */
+      const int len = (k - j < n - i) ? k - j : n - i;
+      if (len > 0 && (j >= i + len || i >= j + len)) {
+        ROW_T *__restrict a = prow + i, *__restrict b = prow + j;
+        int t;
+        for (t = 0; t < len; t++) {
+          const ROW_T x = a[t];
+          a[t] = b[t];
+          b[t] = x;
+        }
+        i += len;
+        j += len;
+      }
+      for (; j < k && i < n && j < n; i++, j++) {
+        const ROW_T t = prow[i];
+        prow[i] = prow[j];
+        prow[j] = t;
+      }
+    }
+  }
+  return 0;
+}
+
+/* chr_null_sums on one thread: four chromosomes' sequential sums interleaved (independent
+   chains, each in the reference's order; four accumulators hide the add latency) */
+static int ROW_CAT(chr_null_sums_1t, ROW_SFX)(const ROW_T *row, double *out, const volatile unsigned *gen,
+                                              unsigned my_gen) {
+  const double *nr = D.nullrow;
+  int c = 0, t, t1, k;
+  for (; c < D.n_chr; c += 4) {
+    const int nc = D.n_chr - c < 4 ? D.n_chr - c : 4;
+    const ROW_T *r[4];
+    double a[4] = {0., 0., 0., 0.};
+    int m = 1 << 30;
+    for (k = 0; k < 4; k++) {
+      r[k] = row + D.chr_start[c + (k < nc ? k : 0)];
+      if (k < nc && D.chr_n[c + k] < m) m = D.chr_n[c + k];
+    }
+    for (t1 = 0; t1 < m; t1 += 8192) {
+      const int te = m - t1 < 8192 ? m : t1 + 8192;
+      double a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+      const ROW_T *r0 = r[0], *r1 = r[1], *r2 = r[2], *r3 = r[3];
+      if (__atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1; /* cancelled */
+      for (t = t1; t < te; t++) { /* chains k >= nc repeat chain 0 and are dropped */
+        a0 += nr[r0[t]];
+        a1 += nr[r1[t]];
+        a2 += nr[r2[t]];
+        a3 += nr[r3[t]];
+      }
+      a[0] = a0; a[1] = a1; a[2] = a2; a[3] = a3;
+    }
+    for (k = 0; k < nc; k++) {
+      for (t = m; t < D.chr_n[c + k]; t++) a[k] += nr[r[k][t]];
+      out[c + k] = a[k];
+    }
+  }
+  return 0;
+}
+
+#undef ROW_CAT
+#undef ROW_CAT2

@@ -134,12 +134,14 @@ typedef struct {
   uint64_t key;
   fh_rowmap_t rm;
   uint32_t *row;  /* row of every site (unpermuted) */
+  void *rowp;     /* the same at the staging width */
+  int rb;         /* staging width: 1, 2 or 4 bytes per row (the narrowest that holds the device rows) */
   int32_t *pos;
   double *nullrow;
   int32_t *chr_start, *chr_n;
   int n_chr;
-  uint32_t *stage[FSCLG_N_SLOTS];  /* one trial's rows, read by every local device (fsclg_host_alloc) */
-  int stage_cap;
+  void *stage[FSCLG_N_SLOTS];  /* one trial's rows (rb bytes each), read by every local device (fsclg_host_alloc) */
+  int stage_cap, stage_rb;
   /* ranks */
   int rank, world;
   fscl_amd_exchange_fn xfn;
@@ -444,6 +446,14 @@ static void prepare(scan_t *s, sm_ptable_t *sm) {
     D.row[i] = fh_row_of(&D.rm, s->snps + i);
     D.pos[i] = s->snps[i].pos;
   }
+  D.rb = D.rm.n_dev_rows <= 0x100 ? 1 : D.rm.n_dev_rows <= 0x10000 ? 2 : 4;
+  free(D.rowp);
+  D.rowp = fh_malloc((size_t)D.rb * (s->n_snps ? s->n_snps : 1), "rows");
+  for (i = 0; i < s->n_snps; i++) {
+    if (D.rb == 1) ((uint8_t *)D.rowp)[i] = (uint8_t)D.row[i];
+    else if (D.rb == 2) ((uint16_t *)D.rowp)[i] = (uint16_t)D.row[i];
+    else ((uint32_t *)D.rowp)[i] = D.row[i];
+  }
   D.n_chr = s->n_chromosomes;
   D.chr_start = fh_malloc(sizeof(int32_t) * D.n_chr, "chr");
   D.chr_n = fh_malloc(sizeof(int32_t) * D.n_chr, "chr");
@@ -453,28 +463,53 @@ static void prepare(scan_t *s, sm_ptable_t *sm) {
   }
   for (l = 0; l < D.n_dev; l++)
     dev_check(fsclg_upload_snps(D.ctx[l], D.pos, D.row, s->n_snps, D.chr_start, D.chr_n, D.n_chr), "upload snps");
-  if (D.stage_cap < s->n_snps) {
+  if (D.stage_cap < s->n_snps || D.stage_rb != D.rb) {
     int k;
     for (k = 0; k < FSCLG_N_SLOTS; k++) {
       fsclg_host_free(D.stage[k]);
-      D.stage[k] = fsclg_host_alloc(sizeof(uint32_t) * (size_t)s->n_snps);
+      D.stage[k] = fsclg_host_alloc((size_t)D.rb * s->n_snps);
       if (!D.stage[k]) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
     }
     D.stage_cap = s->n_snps;
+    D.stage_rb = D.rb;
   }
   D.tab_key = sm; D.snp_key = s->snps; D.n_snps_key = s->n_snps; D.key = key;
 }
 
-/* init_scan_result's window sum (scan-chromosome.c:92-94): sequential from 0.0
-   over the whole chromosome for the given rows */
-static void chr_null_sums(const uint32_t *row, double *out) {
-  int c, i;
-#pragma omp parallel for schedule(dynamic, 1) private(i) if (D.n_chr > 1)
-  for (c = 0; c < D.n_chr; c++) {
-    double acc = 0.;
-    for (i = D.chr_start[c]; i < D.chr_start[c] + D.chr_n[c]; i++) acc += D.nullrow[row[i]];
-    out[c] = acc;
-  }
+/* the row-array routines at each staging width (rows_impl.h), and their dispatch on D.rb */
+#define ROW_T uint8_t
+#define ROW_SFX 8
+#include "rows_impl.h"
+#undef ROW_T
+#undef ROW_SFX
+#define ROW_T uint16_t
+#define ROW_SFX 16
+#include "rows_impl.h"
+#undef ROW_T
+#undef ROW_SFX
+#define ROW_T uint32_t
+#define ROW_SFX 32
+#include "rows_impl.h"
+#undef ROW_T
+#undef ROW_SFX
+
+static void chr_null_sums(const void *row, double *out) {
+  if (D.rb == 1) chr_null_sums_8(row, out);
+  else if (D.rb == 2) chr_null_sums_16(row, out);
+  else chr_null_sums_32(row, out);
+}
+
+static int block_permute(void *prow, const void *row, const snp_t *snps, int n, double nbp, double width_mb,
+                         fh_rand_t *g, unsigned long long *negj, const volatile unsigned *gen, unsigned my_gen) {
+  if (D.rb == 1) return block_permute_8(prow, row, snps, n, nbp, width_mb, g, negj, gen, my_gen);
+  if (D.rb == 2) return block_permute_16(prow, row, snps, n, nbp, width_mb, g, negj, gen, my_gen);
+  return block_permute_32(prow, row, snps, n, nbp, width_mb, g, negj, gen, my_gen);
+}
+
+static int chr_null_sums_1t(const void *row, double *out, const volatile unsigned *gen, unsigned my_gen) {
+  if (D.rb == 1) return chr_null_sums_1t_8(row, out, gen, my_gen);
+  if (D.rb == 2) return chr_null_sums_1t_16(row, out, gen, my_gen);
+  return chr_null_sums_1t_32(row, out, gen, my_gen);
 }
 
 /* contiguous share [lo, hi) of n items for one share index: item i belongs to the
@@ -566,7 +601,7 @@ static int pt_cmp(const void *va, const void *vb) {
 static void set_original_rows(void) {
   double *nul = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
   int l;
-  chr_null_sums(D.row, nul);
+  chr_null_sums(D.rowp, nul);
   for (l = 0; l < D.n_dev; l++) {
     dev_check(fsclg_set_rows(D.ctx[l], NULL), "set rows");
     dev_check(fsclg_set_chr_null(D.ctx[l], nul), "set null sums");
@@ -623,115 +658,19 @@ void scan_chromosome(scan_t *s, sm_ptable_t *sm, int eval_range, int bp_resl, in
 }
 
 /* ------------------------------------------------------------ permutation */
-/* scan-chromosome.c:336-389 on the row array: blocks of consecutive sites
-   (length ~ 1 + Exp(nbp), extended to at least scan_width_mb on the same
-   chromosome) are swapped into place; positions never move.  Q9: a block
-   running past the end is shifted left (j -= k - n) instead of indexing
-   p[-m] as the reference does; such events are counted. */
-static int block_permute(uint32_t *prow, const uint32_t *row, const snp_t *snps, int n, double nbp,
-                         double width_mb, fh_rand_t *g, unsigned long long *negj, const volatile unsigned *gen,
-                         unsigned my_gen) {
-  int i = 0, j, k;
-  const double width = width_mb * 1e6;
-  for (i = 0; i < n; i += 1 << 18) { /* in 1 MB pieces: a cancelled candidate stops soon */
-    if (gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1;
-    memcpy(prow + i, row + i, sizeof(uint32_t) * (size_t)(n - i < (1 << 18) ? n - i : 1 << 18));
-  }
-  i = 0;
-  while (i < n) {
-    const int r1 = fh_rand(g), r2 = fh_rand(g);
-    if (gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1; /* speculation cancelled */
-    j = r1 / (2147483647 + 1.0) * n;
-    if (r2 == 0) k = n; /* Q10: log(0) */
-    else k = j + (int)(-1.0 / nbp * log(r2 / (2147483647 + 1.0)));
-    /* scan-chromosome.c:355-357: extend k while on j's chromosome and within width of
-       pos[j]; positions ascend within a chromosome, so the stop is a lower bound */
-    if (k >= 0 && k < n && snps[k].chr == snps[j].chr) {
-      const int c = snps[j].chr, ce = D.chr_start[c] + D.chr_n[c];
-      const int32_t pj = D.pos[j];
-      int lo = k, hi = ce, step = 1; /* first index in [k, ce) with pos - pj >= width, else ce */
-      while (lo + step < ce && (double)(D.pos[lo + step] - pj) < width) { lo += step; step <<= 1; } /* gallop */
-      if (lo + step < ce) hi = lo + step;
-      if ((double)(D.pos[lo] - pj) < width) lo++; /* lo itself is inside (or is k, unchecked) */
-      while (lo < hi) {
-        const int m = lo + (hi - lo) / 2;
-        if ((double)(D.pos[m] - pj) < width) lo = m + 1; else hi = m;
-      }
-      k = lo;
-    }
-    if (i + (k - j) >= n) k = n;
-    if (k > n) { (*negj)++; j -= k - n; k = n; }
-    {
-      /* scan-chromosome.c:365-372: swap p[i++] with p[j++] while j < k and i < n; disjoint
-         ranges in one vectorisable pass, overlapping ones element by element as written */
-      const int len = (k - j < n - i) ? k - j : n - i;
-      if (len > 0 && (j >= i + len || i >= j + len)) {
-        uint32_t *__restrict a = prow + i, *__restrict b = prow + j;
-        int t;
-        for (t = 0; t < len; t++) {
-          const uint32_t x = a[t];
-          a[t] = b[t];
-          b[t] = x;
-        }
-        i += len;
-        j += len;
-      }
-      for (; j < k && i < n && j < n; i++, j++) {
-        const uint32_t t = prow[i];
-        prow[i] = prow[j];
-        prow[j] = t;
-      }
-    }
-  }
-  return 0;
-}
-
-/* chr_null_sums on one thread: four chromosomes' sequential sums interleaved (independent
-   chains, each in the reference's order; four accumulators hide the add latency) */
-static int chr_null_sums_1t(const uint32_t *row, double *out, const volatile unsigned *gen, unsigned my_gen) {
-  const double *nr = D.nullrow;
-  int c = 0, t, t1, k;
-  for (; c < D.n_chr; c += 4) {
-    const int nc = D.n_chr - c < 4 ? D.n_chr - c : 4;
-    const uint32_t *r[4];
-    double a[4] = {0., 0., 0., 0.};
-    int m = 1 << 30;
-    for (k = 0; k < 4; k++) {
-      r[k] = row + D.chr_start[c + (k < nc ? k : 0)];
-      if (k < nc && D.chr_n[c + k] < m) m = D.chr_n[c + k];
-    }
-    for (t1 = 0; t1 < m; t1 += 8192) {
-      const int te = m - t1 < 8192 ? m : t1 + 8192;
-      double a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
-      const uint32_t *r0 = r[0], *r1 = r[1], *r2 = r[2], *r3 = r[3];
-      if (__atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1; /* cancelled */
-      for (t = t1; t < te; t++) { /* chains k >= nc repeat chain 0 and are dropped */
-        a0 += nr[r0[t]];
-        a1 += nr[r1[t]];
-        a2 += nr[r2[t]];
-        a3 += nr[r3[t]];
-      }
-      a[0] = a0; a[1] = a1; a[2] = a2; a[3] = a3;
-    }
-    for (k = 0; k < nc; k++) {
-      for (t = m; t < D.chr_n[c + k]; t++) a[k] += nr[r[k][t]];
-      out[c + k] = a[k];
-    }
-  }
-  return 0;
-}
+/* block_permute and chr_null_sums_1t: rows_impl.h (scan-chromosome.c:336-389, 92-94) */
 
 /* one trial's rows (in D.stage[slot]) and null sums to the slot on every local device;
    waits until the slot's previous upload has read the staging before it is rewritten */
-static uint32_t *slot_stage(int slot) {
+static void *slot_stage(int slot) {
   int l;
   for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_wait(D.ctx[l], slot), "slot wait");
   return D.stage[slot];
 }
 
-static void slot_upload_buf(int slot, const uint32_t *rows, const double *nul) {
+static void slot_upload_buf(int slot, const void *rows, const double *nul) {
   int l;
-  for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_set_rows_host(D.ctx[l], slot, rows, nul), "set rows");
+  for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_set_rows_packed(D.ctx[l], slot, rows, D.rb, nul), "set rows");
 }
 
 static void slot_upload(int slot, const double *nul) { slot_upload_buf(slot, D.stage[slot], nul); }
@@ -804,7 +743,7 @@ static void sigint_dump(scan_t *s, int n_perm) {
 #define PB_HELD (-3)
 
 typedef struct {
-  uint32_t *buf;   /* one trial's rows, pinned: every local device's upload reads it */
+  void *buf;       /* one trial's rows (D.rb bytes each), pinned: every local device's upload reads it */
   double *nul;     /* its whole-chromosome null sums */
   int owner;       /* the row slot whose upload reads it, or PB_FREE / PB_CAND / PB_HELD */
 } pbuf_t;
@@ -825,7 +764,7 @@ static struct {
   int n;
   double nbp, width_mb;
   pbuf_t pb[FSCLG_N_SLOTS + 2 * SPEC_MAX + 1];
-  int n_pb, pb_cap, pb_nchr;
+  int n_pb, pb_cap, pb_nchr, pb_rb;
 } SP = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
 
 static void *spec_worker(void *arg) {
@@ -847,7 +786,7 @@ static void *spec_worker(void *arg) {
       pthread_mutex_unlock(&SP.mu);
       const double t0 = fh_now();
       for (t = 0; t < d; t++) (void)fh_rand(&r);
-      ok = block_permute(b->buf, D.row, SP.snps, SP.n, SP.nbp, SP.width_mb, &r, &negj, &SP.gen, my) == 0 &&
+      ok = block_permute(b->buf, D.rowp, SP.snps, SP.n, SP.nbp, SP.width_mb, &r, &negj, &SP.gen, my) == 0 &&
            chr_null_sums_1t(b->buf, b->nul, &SP.gen, my) == 0;
       pthread_mutex_lock(&SP.mu);
       SP.running--;
@@ -912,22 +851,23 @@ static void spec_stop(void) {
   SP.n_th = 0;
   SP.stop = 0;
   for (t = 0; t < SP.n_pb; t++) { fsclg_host_free(SP.pb[t].buf); free(SP.pb[t].nul); }
-  SP.n_pb = SP.pb_cap = SP.pb_nchr = 0;
+  SP.n_pb = SP.pb_cap = SP.pb_nchr = SP.pb_rb = 0;
 }
 
 /* buffers for K slots, the candidates and the main thread's own (no job posted) */
 static void pb_reserve(int n_snps, int K) {
   const int want = K + 2 * SP.n_th + 1;
   int b;
-  if (SP.pb_cap < n_snps || SP.pb_nchr < D.n_chr) {
+  if (SP.pb_cap < n_snps || SP.pb_nchr < D.n_chr || SP.pb_rb != D.rb) {
     for (b = 0; b < SP.n_pb; b++) { fsclg_host_free(SP.pb[b].buf); free(SP.pb[b].nul); }
     SP.n_pb = 0;
     SP.pb_cap = n_snps;
     SP.pb_nchr = D.n_chr;
+    SP.pb_rb = D.rb;
   }
   for (; SP.n_pb < want; SP.n_pb++) {
     pbuf_t *p = SP.pb + SP.n_pb;
-    p->buf = fsclg_host_alloc(sizeof(uint32_t) * (size_t)(SP.pb_cap ? SP.pb_cap : 1));
+    p->buf = fsclg_host_alloc((size_t)D.rb * (SP.pb_cap ? SP.pb_cap : 1));
     if (!p->buf) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
     p->nul = fh_malloc(sizeof(double) * (SP.pb_nchr ? SP.pb_nchr : 1), "null sums");
   }
@@ -1218,7 +1158,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     const int slot = (trial + 1) % K;
     trial_batch_t *B = &Bt[slot];
     double tp = fh_now();
-    uint32_t *prow;
+    void *prow;
     tr[0] = tp;
     /* the slot's previous trial: its bulk results (no draws among them) */
     if (B->submitted) {
@@ -1234,7 +1174,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     from_spec = bi >= 0;
     if (bi < 0) {
       bi = pb_get();
-      block_permute(SP.pb[bi].buf, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
+      block_permute(SP.pb[bi].buf, D.rowp, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
     }
     SP.pb[bi].owner = slot;
     prow = SP.pb[bi].buf;
@@ -1407,7 +1347,7 @@ static struct {
   int stop;
   long next, limit, total;  /* local trials j: the next to build; build only j < limit, j < total */
   int nb;                   /* ring of buffers: trial j in buf[j % nb] */
-  uint32_t **buf;
+  void **buf;
   double **nul;
   long *built;              /* the trial each buffer holds, -1 none */
   long q, rank_off, n_perm; /* local trial j -> global trial (j / n_dev) * q + rank_off + j % n_dev */
@@ -1429,7 +1369,7 @@ static void tb_build(long j) {
   if (t <= TB.n_perm) {
     fh_rand_t g;
     fh_srand(&g, tp_trial_seed(g_pseed, t));
-    block_permute(TB.buf[b], D.row, TB.snps, TB.n, TB.nbp, TB.width_mb, &g, &negj, NULL, 0);
+    block_permute(TB.buf[b], D.rowp, TB.snps, TB.n, TB.nbp, TB.width_mb, &g, &negj, NULL, 0);
     chr_null_sums_1t(TB.buf[b], TB.nul[b], &zero, 0);
   }
   pthread_mutex_lock(&TB.mu);
@@ -1525,11 +1465,11 @@ static void permute_throughput(scan_t *s, int n_perm, double permute_nbp, int ev
     const int want = spec_threads_wanted();
     TB.nb = (K + 1) * nd + want;
     TB.limit = TB.nb;
-    TB.buf = fh_calloc((size_t)TB.nb, sizeof(uint32_t *), "permutation ring");
+    TB.buf = fh_calloc((size_t)TB.nb, sizeof(void *), "permutation ring");
     TB.nul = fh_calloc((size_t)TB.nb, sizeof(double *), "permutation ring");
     TB.built = fh_malloc(sizeof(long) * (size_t)TB.nb, "permutation ring");
     for (i = 0; i < TB.nb; i++) {
-      TB.buf[i] = fsclg_host_alloc(sizeof(uint32_t) * (size_t)(s->n_snps ? s->n_snps : 1));
+      TB.buf[i] = fsclg_host_alloc((size_t)D.rb * (s->n_snps ? s->n_snps : 1));
       if (!TB.buf[i]) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
       TB.nul[i] = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
       TB.built[i] = -1;
@@ -1575,7 +1515,7 @@ static void permute_throughput(scan_t *s, int n_perm, double permute_nbp, int ev
         bi = tb_get(j);
         D.st.host_perm_s += fh_now() - tp;
         tp = fh_now();
-        dev_check(fsclg_slot_set_rows_host(D.ctx[l], slot, TB.buf[bi], TB.nul[bi]), "set rows");
+        dev_check(fsclg_slot_set_rows_packed(D.ctx[l], slot, TB.buf[bi], D.rb, TB.nul[bi]), "set rows");
         D.st.host_upload_s += fh_now() - tp;
         dev_check(fsclg_slot_windows(D.ctx[l], slot, b->cells, b->n, eval_range), "window sums");
         dev_check(fsclg_search_submit(D.ctx[l], 2 + slot, slot, b->cells, b->n, eval_range, bp_resl), "search submit");
@@ -1632,7 +1572,7 @@ static void permute_throughput(scan_t *s, int n_perm, double permute_nbp, int ev
 void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, double alpha_factor, int n_threads,
                   int eval_range, int bp_resl, int large_grid_sp, double scan_width_mb) {
   fh_rand_t *g = perm_rng();
-  uint32_t *prow;
+  void *prow;
   int *act, n_act = s->n_scan_pts, i, k, trial = -1;
   const int save = CLR_NULL_DIST_SAVE; /* scan-chromosome.c:496 */
   fsclg_cell_t *cells;
@@ -1675,7 +1615,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   for (;;) {
     double tp = fh_now();
     prow = slot_stage(0);
-    block_permute(prow, D.row, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
+    block_permute(prow, D.rowp, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
     D.st.host_perm_s += fh_now() - tp;
     trial++;
     for (i = k = 0; i < n_act; i++)
@@ -1982,7 +1922,8 @@ void fscl_amd_shutdown(void) {
   free(DI.null_full); free(DI.null_seen); free(DI.pos); free(DI.row); free(DI.tpos); free(DI.trow);
   free_rowmap(&DI.rm);
   memset(&DI, 0, sizeof DI);
-  free(D.row); free(D.pos); free(D.chr_start); free(D.chr_n); free(D.nullrow);
+  free(D.row); free(D.pos); free(D.chr_start); free(D.chr_n); free(D.nullrow); free(D.rowp);
+  D.rowp = NULL;
   D.row = NULL; D.pos = NULL; D.chr_start = NULL; D.chr_n = NULL; D.nullrow = NULL;
   free_rowmap(&D.rm);
   if (D.sim) { fclose(D.sim); D.sim = NULL; }

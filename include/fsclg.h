@@ -140,6 +140,9 @@ void *fsclg_host_alloc(size_t bytes);
 void fsclg_host_free(void *p);
 int fsclg_slot_wait(fsclg_ctx *c, int slot);
 int fsclg_slot_set_rows_host(fsclg_ctx *c, int slot, const uint32_t *row, const double *chr_null);
+/* the same with rows of row_bytes = 1, 2 or 4 bytes each (1: n_rows <= 256, 2: n_rows <= 65536):
+   a narrower staging is fewer PCIe bytes for every device's upload of every trial */
+int fsclg_slot_set_rows_packed(fsclg_ctx *c, int slot, const void *row, int row_bytes, const double *chr_null);
 
 /* sequential window null sums (init_scan_result's sum from 0.0) for each chromosome's
    whole-chromosome window, for the rows currently set */
