@@ -7,11 +7,15 @@
 #define ROW_CAT(a, b) ROW_CAT2(a, b)
 
 /* init_scan_result's window sum (scan-chromosome.c:92-94): sequential from 0.0 over the
-   whole chromosome for the given rows */
+   whole chromosome for the given rows, for the chromosomes whose window is the whole
+   chromosome (D.chr_list; the others' entries are never read and are set to 0) */
 static void ROW_CAT(chr_null_sums, ROW_SFX)(const ROW_T *row, double *out) {
-  int c, i;
-#pragma omp parallel for schedule(dynamic, 1) private(i) if (D.n_chr > 1)
-  for (c = 0; c < D.n_chr; c++) {
+  const int nl = D.chr_list ? D.n_chr_list : D.n_chr;
+  int q, i;
+  if (D.chr_list) for (q = 0; q < D.n_chr; q++) out[q] = 0.;
+#pragma omp parallel for schedule(dynamic, 1) private(i) if (nl > 1)
+  for (q = 0; q < nl; q++) {
+    const int c = D.chr_list ? D.chr_list[q] : q;
     double acc = 0.;
     for (i = D.chr_start[c]; i < D.chr_start[c] + D.chr_n[c]; i++) acc += D.nullrow[row[i]];
     out[c] = acc;
@@ -86,15 +90,18 @@ static int ROW_CAT(block_permute, ROW_SFX)(ROW_T *prow, const ROW_T *row, const 
 static int ROW_CAT(chr_null_sums_1t, ROW_SFX)(const ROW_T *row, double *out, const volatile unsigned *gen,
                                               unsigned my_gen) {
   const double *nr = D.nullrow;
-  int c = 0, t, t1, k;
-  for (; c < D.n_chr; c += 4) {
-    const int nc = D.n_chr - c < 4 ? D.n_chr - c : 4;
+  const int nl = D.chr_list ? D.n_chr_list : D.n_chr;
+  int q = 0, t, t1, k, cc[4];
+  if (D.chr_list) for (k = 0; k < D.n_chr; k++) out[k] = 0.;
+  for (; q < nl; q += 4) {
+    const int nc = nl - q < 4 ? nl - q : 4;
     const ROW_T *r[4];
     double a[4] = {0., 0., 0., 0.};
     int m = 1 << 30;
     for (k = 0; k < 4; k++) {
-      r[k] = row + D.chr_start[c + (k < nc ? k : 0)];
-      if (k < nc && D.chr_n[c + k] < m) m = D.chr_n[c + k];
+      cc[k] = D.chr_list ? D.chr_list[q + (k < nc ? k : 0)] : q + (k < nc ? k : 0);
+      r[k] = row + D.chr_start[cc[k]];
+      if (k < nc && D.chr_n[cc[k]] < m) m = D.chr_n[cc[k]];
     }
     for (t1 = 0; t1 < m; t1 += 8192) {
       const int te = m - t1 < 8192 ? m : t1 + 8192;
@@ -110,8 +117,8 @@ static int ROW_CAT(chr_null_sums_1t, ROW_SFX)(const ROW_T *row, double *out, con
       a[0] = a0; a[1] = a1; a[2] = a2; a[3] = a3;
     }
     for (k = 0; k < nc; k++) {
-      for (t = m; t < D.chr_n[c + k]; t++) a[k] += nr[r[k][t]];
-      out[c + k] = a[k];
+      for (t = m; t < D.chr_n[cc[k]]; t++) a[k] += nr[r[k][t]];
+      out[cc[k]] = a[k];
     }
   }
   return 0;

@@ -136,6 +136,9 @@ typedef struct {
   uint32_t *row;  /* row of every site (unpermuted) */
   void *rowp;     /* the same at the staging width */
   int rb;         /* staging width: 1, 2 or 4 bytes per row (the narrowest that holds the device rows) */
+  int *chr_list;  /* permutation trials: the chromosomes whose null sum is read (window = whole chromosome,
+                     n <= 2 eval_range + 1, init_scan_result); NULL: every chromosome */
+  int n_chr_list;
   int32_t *pos;
   double *nullrow;
   int32_t *chr_start, *chr_n;
@@ -1597,6 +1600,12 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
     if (e && !strncmp(e, "throughput", 10)) fscl_amd_set_permute_mode(FSCL_AMD_PERMUTE_THROUGHPUT,
                                                                        e[10] == ':' ? strtoull(e + 11, NULL, 0) : g_pseed);
   }
+  /* a trial's whole-chromosome null sums are read only where the window is the whole chromosome
+     (scan-chromosome.c:75-94): the other chromosomes' sums are not computed */
+  D.chr_list = fh_malloc(sizeof(int) * (D.n_chr ? D.n_chr : 1), "chromosomes");
+  D.n_chr_list = 0;
+  for (i = 0; i < D.n_chr; i++)
+    if ((long long)D.chr_n[i] <= 2ll * eval_range + 1) D.chr_list[D.n_chr_list++] = i;
   if (g_pmode == FSCL_AMD_PERMUTE_THROUGHPUT) { /* the rand() stream is not used */
     permute_throughput(s, n_perm, permute_nbp, eval_range, bp_resl, large_grid_sp, scan_width_mb, save);
     goto done;
@@ -1661,6 +1670,9 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
 done:
   cr_logmsg(MSG_STATUS, "Scanning snp block permutations... finished.\n");
   signal(SIGINT, SIG_DFL);
+  free(D.chr_list);
+  D.chr_list = NULL;
+  D.n_chr_list = 0;
   set_original_rows();
   D.st.permute_s += fh_now() - t0;
 }

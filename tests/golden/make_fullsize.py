@@ -18,6 +18,7 @@ Cases (SURVEY §8(d) / BASELINE.json):
   C5_chr_p200 one C5 chromosome, --n-permute=200 (early prune)    (configs[4] regime)
   C4_bench_p1000  bench.py's default job exactly (seed 1), --n-permute=1000 (configs[3], the metric's job)
   C5_full_p25 the C5 genome (seed 55), --n-permute=25 (windowed null sums per trial, first prunes)
+  C2_bench_p100, C3_bench_p100  bench.py --config C2 / C3 exactly (seed 1, 100 permutations)
 """
 from __future__ import annotations
 
@@ -53,6 +54,13 @@ CASES = {
     # the first prune draws (permute_p reaches 20 only after 20 trials)
     "C5_full_p25": dict(gen=dict(n_chr=22, chr_len=227_272_727, snps_per_chr=227_273, n=400, folded=0.0, seed=55,
                                  sweeps_per_chr=2), opts=["--n-permute=25"]),
+    # bench.py --config C2 / C3, exactly (seed 1, 100 permutations; C3 with its ascertainment
+    # options): their bench lines check every timed job against these digests too
+    "C2_bench_p100": dict(gen=dict(n_chr=1, chr_len=200_000_000, snps_per_chr=100_000, n=100, folded=0.0, seed=1,
+                                   sweeps_per_chr=2), opts=["--n-permute=100"]),
+    "C3_bench_p100": dict(gen=dict(n_chr=1, chr_len=200_000_000, snps_per_chr=100_000, n=100, folded=0.3, seed=1,
+                                   sweeps_per_chr=2),
+                          opts=["--n-permute=100", "--asc-depth=20", "--asc-minimum-freq=2"]),
 }
 
 

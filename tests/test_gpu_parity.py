@@ -352,6 +352,26 @@ def test_window_sum_kernels_match_oracle(built, tmp, monkeypatch, mode, er):
     assert fscl_amd.get_stats()["window_ms"] > 0
 
 
+def test_mixed_window_and_whole_chromosome_sums_match_oracle(built, tmp):
+    """One chromosome longer than the window (8000 SNPs, 2*300+1-site windows: device window
+    sums) and one shorter (400 SNPs: the window is the whole chromosome, whose null sum the host
+    computes per trial -- only for such chromosomes, scan-chromosome.c:75-94), with
+    permutations: bit-identical to the oracle."""
+    snp = tmp / "mixed.snp"
+    chroms = synth.generate(n_chr=1, chr_len=8_000_000, snps_per_chr=8000, n=60, seed=95, sweeps_per_chr=1,
+                            chr_names=["chrA"])
+    chroms += synth.generate(n_chr=1, chr_len=400_000, snps_per_chr=400, n=60, seed=96, sweeps_per_chr=1,
+                             chr_names=["chrB"])
+    synth.write_snp_file(str(snp), chroms)
+    opts = ["--coarse-grid-spacing=100000", "--n-permute=25", "--eval-range=300"]
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
+    kw = _kw([o for o in opts if not o.startswith("--eval-range=")])
+    kw["eval_range"] = 300
+    scan = fscl_amd.run(snp, tmp / "g.txt", **kw)
+    assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), "mixed windows")
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+
+
 def _fullsize():
     import json
     return json.loads((GOLD / "fullsize.json").read_text())
