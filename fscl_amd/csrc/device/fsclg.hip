@@ -67,8 +67,12 @@ constexpr int NWAVE = WG / 64;
 #define FSCLG_SEG 4096
 #endif
 constexpr int SEG = FSCLG_SEG;     // terms per work segment
-constexpr int SEG_SPLIT = 1024;    // split cells (latency): finer segments spread over the members' waves
+#ifndef FSCLG_SEG_SPLIT
+#define FSCLG_SEG_SPLIT 1024
+#endif
+constexpr int SEG_SPLIT = FSCLG_SEG_SPLIT;  // split cells (latency): finer segments spread over the members' waves
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
+constexpr int MAXWALK_SPLIT = 64;  // split cells: 2 points x (11 coarse + 15 speculative refine candidates)
 constexpr int MAXSEG_W = (163841 / SEG_SPLIT + 4 + 31) / 32 * 32;  // segments per walk (165 at 163841 terms, split;
                                                                   // each part's ends are 128-site aligned)
 constexpr int SEGWORDS = MAXSEG_W / 32;
@@ -152,12 +156,19 @@ struct Params {
                                // beside the current one (FSCLG_LOOKAHEAD=0: one point per search;
                                // 2: mispredict on purpose, the fallback path's test)
   int split;                   // members per cell (1: one workgroup per cell)
+  int spec_refine;             // split cells: evaluate the refine walks of a guessed coarse winner beside the
+                               // coarse walks (one phase per alpha search when the guess holds)
+  int ci_guess;                // the guess for points with no evaluated neighbour (the recent results' mode)
   char* xacc;                  // [n_cells][2] XAcc
   unsigned int* xcnt;          // [n_cells] arrivals
 };
 
 struct Pt {                     // one scan point being evaluated (scan_pt_t subset)
   int chr, nearest, sweep, wstart, wend, n_snps, flags, pad;
+  int ci;                        // its alpha search's coarse winner (n_coarse: none beat the initial state)
+  int sg;                        // split cells: the coarse winner guessed before the search (speculative refine)
+  int spad;                      // split cells: (first << 8) | count of the speculative refine walks
+  int pad2;
   double N, inv_u, u, la, sm, clr;
 };
 
@@ -175,33 +186,37 @@ struct Walk {
   int pad_;
 };
 
-struct Smem {
+template <int MW>
+struct SmemT {
+  static constexpr int MAXW = MW;
   Pt pt[4];                       // cells: start, end, midpoint, the midpoint's predicted child
-  Walk w[MAXWALK];
-  unsigned long long P[MAXWALK];
-  unsigned long long Q[MAXWALK];
-  double Pd[MAXWALK], Qd[MAXWALK];  // fp64 sums of the lanes whose accumulators passed 2^51 (approximate)
-  unsigned int segbits[MAXWALK][SEGWORDS];
-  int wflag[MAXWALK];
-  int exact[MAXWALK];
-  double val[MAXWALK];
-  double appr[MAXWALK];
-  double bnd[MAXWALK];
+  Walk w[MW];
+  unsigned long long P[MW];
+  unsigned long long Q[MW];
+  double Pd[MW], Qd[MW];  // fp64 sums of the lanes whose accumulators passed 2^51 (approximate)
+  unsigned int segbits[MW][SEGWORDS];
+  int wflag[MW];
+  int exact[MW];
+  double val[MW];
+  double appr[MW];
+  double bnd[MW];
   int ties[MAXTIES];
   int n_ties;
   int seg_total;
   int nwalk;
-  int need_slow[MAXWALK];
+  int need_slow[MW];
   int n_slow;
   int best[3];
   unsigned long long cnt[8];
   int ivc0;                       // base interval of the coefficient window now in LDS
   int ngrp;                       // walk groups of the phase (one LDS window each), in segment order
-  int gwb[MAXWALK];
-  int gseg[MAXWALK + 1];
-  int word[MAXWALK];              // walks in segment order
+  int gwb[MW];
+  int gseg[MW + 1];
+  int word[MW];              // walks in segment order
   int hkey;                       // interval-histogram key of the phase: 0 coarse, 1 + c refine around coarse c
-  unsigned long long tph[4];      // FSCLG_PHASE_TIMING: wall-clock ticks in bounds / layout / segments / resolve
+  int hitmask;                    // split cells: the points whose speculative refine walks were the right ones
+  unsigned long long tph[5];      // FSCLG_PHASE_TIMING: wall-clock ticks in bounds / layout / segments / resolve,
+                                  // and (slot 4) the split combine's wait for the other members' arrival
   int cell, member;               // split cells: this workgroup's cell and member index
   int inst;                       // split cells: eval_walks instances so far (the XAcc region in turn)
   int xbase;                      // split cells: this member's first tie slot
@@ -209,6 +224,9 @@ struct Smem {
   int iev;                        // FSCLG_INST_TRACE: events recorded so far
   int xnt[8];                     // split cells: each member's tie count of the instance
 };
+using Smem = SmemT<MAXWALK>;             // the throughput kernel (its LDS window takes the rest)
+using SmemSplit = SmemT<MAXWALK_SPLIT>;  // split cells: room for speculative refine walks (no LDS window)
+
 
 // FSCLG_INST_TRACE (development aid): thread 0 of cell 0's first member records timestamped
 // events (tag, a, b) after the per-cell trace area: [count, then 4 words per event]
@@ -233,10 +251,10 @@ struct Smem {
 constexpr int MAXSPLIT = 8;
 constexpr int XTIES = MAXTIES / MAXSPLIT;  // tie slots per member (more: the overflow path)
 struct XAcc {
-  unsigned long long P[MAXSPLIT][MAXWALK], Q[MAXSPLIT][MAXWALK];
-  double Pd[MAXSPLIT][MAXWALK], Qd[MAXSPLIT][MAXWALK];
-  unsigned int wflag[MAXSPLIT][MAXWALK];
-  unsigned int segbits[MAXSPLIT][MAXWALK][SEGWORDS];
+  unsigned long long P[MAXSPLIT][MAXWALK_SPLIT], Q[MAXSPLIT][MAXWALK_SPLIT];
+  double Pd[MAXSPLIT][MAXWALK_SPLIT], Qd[MAXSPLIT][MAXWALK_SPLIT];
+  unsigned int wflag[MAXSPLIT][MAXWALK_SPLIT];
+  unsigned int segbits[MAXSPLIT][MAXWALK_SPLIT][SEGWORDS];
   unsigned int nt[MAXSPLIT];
   int ties[MAXSPLIT][XTIES];
 };
@@ -288,8 +306,8 @@ __device__ __forceinline__ double log_ad_of(int i, int sweep, double la, const P
 // division: an fma estimate lowered by 1e-9 (its error and the reference's rounding are
 // ~1e-13) is the interval or the one below it, and the exact threshold of the next one
 // settles it (thr[n_iv] = +inf: the reference clamps at n_iv - 1)
-template <bool LDS>
-__device__ __forceinline__ int interval_of(double x, const Smem& S, const Params& P) {
+template <bool LDS, class SM>
+__device__ __forceinline__ int interval_of(double x, const SM& S, const Params& P) {
   // x >= LOG_AD_MIN (log_table >= 0 and every alpha >= LOG_AD_MIN, checked by
   // fsclg_set_alpha_grid), so the estimate is >= -1e-9 and truncates to >= 0
   int iv = (int)__builtin_fma(x, P.inv_step, P.iv_off);
@@ -300,8 +318,8 @@ __device__ __forceinline__ int interval_of(double x, const Smem& S, const Params
   return iv + (x >= hi ? 1 : 0);
 }
 
-template <bool LDS>
-__device__ __forceinline__ double null_of(uint32_t r, const Smem& S, const Params& P) {
+template <bool LDS, class SM>
+__device__ __forceinline__ double null_of(uint32_t r, const SM& S, const Params& P) {
   if constexpr (LDS) return reinterpret_cast<const double*>(fsclg_dyn + P.off_nul)[r];
   else return P.nullrow[r];
 }
@@ -325,8 +343,8 @@ __device__ __forceinline__ void coef_ld(const char* base, uint32_t off, const Pa
 // the coefficient block of (row, interval) into a = (c0, c1), b = (c2, c3): from the LDS
 // window when (interval, row) lies in it (every row of intervals [ivc0, ivc0 + n_civ)),
 // from the global table otherwise
-template <bool LDS>
-__device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, const Params& P, double2& a, double2& b) {
+template <bool LDS, class SM>
+__device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const SM& S, const Params& P, double2& a, double2& b) {
   if constexpr (LDS) {
     const uint32_t ci = (uint32_t)(iv - S.ivc0);
     const bool hit = ci < (uint32_t)P.n_civ;  // every row is cached
@@ -339,8 +357,8 @@ __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const Smem& S, co
 
 // coefficients of U terms: the intervals of all U first (their threshold reads overlap),
 // then per term the LDS window or, for lanes outside it, the global table
-template <bool LDS, int U>
-__device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t (&rv)[U], const Smem& S,
+template <bool LDS, int U, class SM>
+__device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t (&rv)[U], const SM& S,
                                            const Params& P, int ivc0, double2 (&ca)[U], double2 (&cb)[U],
                                            int (&iv)[U]) {
   constexpr bool CACHE = LDS;
@@ -363,8 +381,8 @@ __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t 
 }
 
 // snp_likelihood (sm-search.c:85-103) with spline_interpolate (sm-spline.c:48-60)
-template <bool LDS>
-__device__ __forceinline__ double term_dev(int i, int sweep, double la, const Smem& S, const Params& P) {
+template <bool LDS, class SM>
+__device__ __forceinline__ double term_dev(int i, int sweep, double la, const SM& S, const Params& P) {
   const double x = log_ad_of(i, sweep, la, P);
   const int iv = interval_of<LDS>(x, S, P);
   const uint32_t r = P.pr[phys(i)].y;
@@ -459,8 +477,8 @@ __device__ __forceinline__ void set_binade(Pt& pt) {
 // is inside: inside on a prefix of (near + 1, wend + 1)).  logt is nondecreasing in |d|, so
 // log(alpha d) > 4 is |d| >= dfail, an integer compare per probe (no log-table gather in the
 // search's dependent rounds; the host derives dfail from the same table and adds).
-template <int G>
-__device__ __forceinline__ void walk_bounds_g(Smem& S, const Params& P, int tid, int nw) {
+template <int G, class SM>
+__device__ __forceinline__ void walk_bounds_g(SM& S, const Params& P, int tid, int nw) {
   const int lane = tid & 63, g = tid / G;
   const bool act = g < 2 * nw;
   const int w = act ? g >> 1 : 0, side = g & 1;
@@ -495,9 +513,11 @@ __device__ __forceinline__ void walk_bounds_g(Smem& S, const Params& P, int tid,
   }
 }
 
-__device__ __forceinline__ void walk_bounds_par(Smem& S, const Params& P, int tid, int nw) {
+template <class SM>
+__device__ __forceinline__ void walk_bounds_par(SM& S, const Params& P, int tid, int nw) {
   if (2 * nw * 16 <= WG) walk_bounds_g<16>(S, P, tid, nw);  // uniform over the workgroup
-  else walk_bounds_g<8>(S, P, tid, nw);
+  else if (2 * nw * 8 <= WG) walk_bounds_g<8>(S, P, tid, nw);
+  else walk_bounds_g<4>(S, P, tid, nw);  // split cells' speculative phases (up to 64 walks)
 }
 
 // exact sequential sum of one walk by one wave (slow path, settles an argmax), 64 terms at
@@ -534,8 +554,8 @@ __device__ __forceinline__ double exact_chunk_add(double acc, double t, int lim)
   return acc;
 }
 
-template <bool LDS>
-__device__ __forceinline__ double walk_sequential(const Smem& S, const Walk& W, const Pt& pt, const Params& P, int lane) {
+template <bool LDS, class SM>
+__device__ __forceinline__ double walk_sequential(const SM& S, const Walk& W, const Pt& pt, const Params& P, int lane) {
   double acc = pt.N;
   for (int kb = 0; kb < W.len; kb += 64) {
     const int k = kb + lane;
@@ -617,8 +637,8 @@ __device__ __forceinline__ double uniform_f64(double v) {
 // window or the global table, a uniform branch).  Otherwise the trip takes the per-lane path
 // of run_segment and re-centres civ on its last site.  Only the final trip of a segment
 // masks lanes past its end (zero sentinel row).
-template <bool LDS, int SEGN, int U>
-__device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, const Params& P, int lane,
+template <bool LDS, int SEGN, int U, class SM>
+__device__ __forceinline__ void run_segment_idx(SM& S, int w, int s, int s1, const Params& P, int lane,
                                                 double& acc, double& accm) {
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[W.p];
@@ -816,7 +836,8 @@ __device__ __forceinline__ void run_segment_idx(Smem& S, int w, int s, int s1, c
 // a wave's share of walk w: int64 totals of sum R and sum |R| into S.P / S.Q.  Exact when
 // every lane's |R| total is below 2^51 (then all fp64 partials were exact, fl being
 // monotone; NaN fails the test); 8 waves x 64 lanes keep the walk's totals below 2^60.
-__device__ __forceinline__ void flush_walk(Smem& S, int w, double acc, double accm, int lane) {
+template <class SM>
+__device__ __forceinline__ void flush_walk(SM& S, int w, double acc, double accm, int lane) {
   const bool big = !(accm < 2251799813685248.0);  // 2^51
   const long long isum = wave_sum64(big ? 0 : (long long)acc);
   const long long imag = wave_sum64(big ? 0 : (long long)accm);
@@ -840,8 +861,8 @@ __device__ __forceinline__ void flush_walk(Smem& S, int w, double acc, double ac
 // resolve walk w's exact value (thread per walk).  S.P = sum R, S.Q = sum |R| over the walk.
 // Ties are replayed in k order: fl(acc + t) rounds to even, so where t/u = F + 1/2 an odd
 // running sum takes the other neighbour of the even R (+1 if R = F, -1 if R = F + 1).
-template <int SEGN>
-__device__ __forceinline__ void resolve_walk(Smem& S, int w) {
+template <int SEGN, class SM>
+__device__ __forceinline__ void resolve_walk(SM& S, int w) {
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[W.p];
   if (W.len == 0) { S.exact[w] = 1; S.val[w] = pt.N; return; }
@@ -850,7 +871,7 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
   const bool overflow = S.n_ties > MAXTIES;
   int T = 0;
   const int nt = S.n_ties < MAXTIES ? S.n_ties : MAXTIES;
-  for (int j = 0; j < nt; j++) T += (((S.ties[j] >> 20) & 31) == w);
+  for (int j = 0; j < nt; j++) T += (((S.ties[j] >> 20) & 63) == w);
   const bool big = S.wflag[w] != 0 || pt.inv_u == 0.0;
   const long long S0 = pt.inv_u == 0.0 ? 0 : (long long)(pt.N * pt.inv_u);
   const long long LO = -(1ll << 53), HI = -((1ll << 52) + 1);
@@ -877,7 +898,7 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
         const int v = S.ties[j];
         const int jj = v & 0x3FFFF;
         const int k = jj <= nl ? nl - jj : jj;
-        if (((v >> 20) & 31) == w && k > prevk && k < bestk) { bestk = k; bestv = v; }
+        if (((v >> 20) & 63) == w && k > prevk && k < bestk) { bestk = k; bestv = v; }
       }
       prevk = bestk;
       // parity of the running sum before this term: S0, then the terms before it in k
@@ -926,7 +947,8 @@ __device__ __forceinline__ void resolve_walk(Smem& S, int w) {
 // stage the coefficient blocks of intervals [wb, wb + n_civ) x every row into LDS, in the
 // table's own [iv][row][4] layout: one contiguous copy (all threads; the caller brackets
 // it with barriers)
-__device__ __forceinline__ void load_window(Smem& S, const Params& P, int wb) {
+template <class SM>
+__device__ __forceinline__ void load_window(SM& S, const Params& P, int wb) {
   double2* dst = reinterpret_cast<double2*>(fsclg_dyn);
   const double2* src = reinterpret_cast<const double2*>(P.coef) + (size_t)wb * P.stride * 2;
   for (int e = threadIdx.x; e < 2 * P.n_cache; e += WG) dst[e] = src[e];
@@ -958,7 +980,8 @@ __device__ __forceinline__ unsigned long long ag_xchg64(unsigned long long* p, u
 // argmax and bisection then run redundantly and agree).  Three memory round trips: the
 // stores' completion, the arrival, the reads.  A member that waits longer than ~1 s (the
 // others never started: not co-resident) flags the cell and goes on.
-__device__ __forceinline__ void combine_members(Smem& S, const Params& P, int nw) {
+template <class SM>
+__device__ __forceinline__ void combine_members(SM& S, const Params& P, int nw) {
   const int tid = threadIdx.x;
   const int inst = S.inst, me = S.member, G = P.split;
   XAcc* R = reinterpret_cast<XAcc*>(P.xacc + ((size_t)S.cell * 2 + (size_t)(inst & 1)) * sizeof(XAcc));
@@ -991,6 +1014,9 @@ __device__ __forceinline__ void combine_members(Smem& S, const Params& P, int nw
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > 100000000ull) { S.xfail = PF_SPLIT_TIMEOUT; break; }  // ~1 s at 100 MHz
     }
+#ifdef FSCLG_PHASE_TIMING
+    S.tph[4] += wall_clock64() - t0;
+#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -1049,8 +1075,8 @@ __device__ __forceinline__ void combine_members(Smem& S, const Params& P, int nw
   __syncthreads();
 }
 
-template <bool LDS, bool SPLIT>
-__device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
+template <bool LDS, bool SPLIT, class SM>
+__device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
   constexpr int SEGN = SPLIT ? SEG_SPLIT : SEG;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nw = __builtin_amdgcn_readfirstlane(S.nwalk);
@@ -1072,7 +1098,7 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
   PHASE_MARK(0);  // FSCLG_PHASE_TIMING slots: 0 bounds + layout, 1 wave 0's segments, 2 the wait for
                   // the other waves, 3 the members' combine + resolve
   TRACE("  bounds done: nw=%d w0 len=%d nl=%d nr=%d\n", nw, S.w[0].len, S.w[0].nl, S.w[0].nr);
-  // layout by wave 0, one lane per walk (nw <= MAXWALK = 32), values in registers
+  // layout by wave 0, one lane per walk (nw <= 64), values in registers
   if (wave == 0) {
     const bool act = lane < nw;
     const int K = P.n_civ;
@@ -1186,7 +1212,8 @@ __device__ __forceinline__ void eval_walks(Smem& S, const Params& P) {
 // winning walk, PRIOR if nothing beats the prior, or AMBIG after marking every
 // inexact candidate that could still win for the sequential slow path.
 constexpr int PRIOR = -1, AMBIG = -2;
-__device__ __forceinline__ int argmax_or_mark(Smem& S, int first, int count, double prior_val) {
+template <class SM>
+__device__ __forceinline__ int argmax_or_mark(SM& S, int first, int count, double prior_val) {
   int bi = PRIOR;
   double bv = prior_val;
   for (int c = first; c < first + count; c++)
@@ -1212,7 +1239,8 @@ __device__ __forceinline__ double wave_max_f64(double v) {
 // loop's winner is the first exact candidate holding the largest exact value above the prior
 // (strict '>': a later equal value never replaces it; NaN never wins); the best lower bound and
 // the marks as there.  Every lane returns the result.
-__device__ __forceinline__ int argmax_wave(Smem& S, int first, int count, double prior_val, int lane) {
+template <class SM>
+__device__ __forceinline__ int argmax_wave(SM& S, int first, int count, double prior_val, int lane) {
   const bool in = lane < count;
   const int c = first + (in ? lane : 0);
   const bool ex = in && S.exact[c] != 0;
@@ -1232,34 +1260,74 @@ __device__ __forceinline__ int argmax_wave(Smem& S, int first, int count, double
   return __ballot(mark) ? AMBIG : bi;
 }
 
-// search_maxalpha for the points in slots [p0, p0+np) (sm-search.c:269-300)
-template <bool LDS, bool SPLIT = false>
-__device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, int p0, int np) {
+// search_maxalpha for the points in slots [p0, p0+np) (sm-search.c:269-300): the coarse phase (11
+// alpha, strict '>' from -DBL_MAX), then the refine phase around the coarse winner (14-15 alpha,
+// strict '>' from the coarse best).  Split cells (latency-bound: every phase is a chain of walk
+// bounds, segments, the members' combine and the argmax) may evaluate the refine walks of a
+// GUESSED coarse winner (Pt::sg) in the coarse phase: for a point whose real coarse winner is the
+// guess, those walks are exactly the refine phase's walks (same alpha, same exact sums), so its
+// refine argmax runs on them at once; only the points whose guess missed take a second phase.
+// The candidates, their values and the order of the strict '>' comparisons are the reference's
+// either way; a wrong guess costs only its walks.
+template <bool LDS, bool SPLIT = false, class SM>
+__device__ __forceinline__ void search_maxalpha_pts(SM& S, const Params& P, int p0, int np) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nc = P.n_coarse;
+  const bool spec = SPLIT && P.spec_refine && np * (nc + MAXREF) <= SM::MAXW;  // uniform
   if (tid < np) set_binade(S.pt[p0 + tid]);
   IEV(0, np, S.pt[p0].sweep);  // an alpha search starts
   TRACE("maxalpha: p0=%d np=%d sweep=%d N=%g\n", p0, np, S.pt[p0].sweep, S.pt[p0].N);
   // ---- coarse phase
-  if (tid < np * P.n_coarse) {
-    const int p = tid / P.n_coarse, a = tid % P.n_coarse;
+  if (tid < np * nc) {
+    const int p = tid / nc, a = tid % nc;
     S.w[tid].p = p0 + p;
     S.w[tid].la = P.la_coarse[a];
     S.w[tid].dfail = P.dfail[a];
     S.w[tid].len = 0; S.w[tid].nl = S.w[tid].nr = 0;
   }
-  if (tid == 0) { S.nwalk = np * P.n_coarse; S.cnt[3] += np; S.hkey = 0; }
+  if (tid == 0) { S.nwalk = np * nc; S.cnt[3] += np; S.hkey = 0; }
+  // refine walks for point p's list ci[p] (lane p), after the first `base` walks: wave 0, lane
+  // p * MAXREF + r for walk r; returns (first << 8) | count of point p's walks in lane p and sets
+  // S.nwalk (cnt[p] = 0: none for that point)
+  auto lay_refine = [&](int ci, int cnt, int base) {
+    int off = 0, nw = base;
+    for (int p = 0; p < np; p++) {  // np <= 2, uniform
+      const int cp = __builtin_amdgcn_readlane(cnt, p);
+      if (lane == p) off = nw;
+      nw += cp;
+    }
+    if (lane == 0) S.nwalk = nw;
+    const int p = lane / MAXREF, r = lane % MAXREF;
+    const int pc = p < np ? p : 0;
+    const int cip = __shfl(ci, pc, 64), cntp = __shfl(cnt, pc, 64), offp = __shfl(off, pc, 64);
+    if (p < np && r < cntp) {
+      Walk& V = S.w[offp + r];
+      V.p = p0 + p;
+      V.la = P.la_refine[cip * MAXREF + r];
+      V.dfail = P.dfail[nc + cip * MAXREF + r];
+      V.len = 0; V.nl = V.nr = 0;
+    }
+    return (off << 8) | cnt;
+  };
+  if (spec && wave == 0) {  // the guessed winners' refine walks, after the coarse walks
+    int g = 0, cnt = 0;
+    if (lane < np) { g = min(max(S.pt[p0 + lane].sg, 0), nc); cnt = P.n_refine[g]; }
+    const int pad = lay_refine(g, cnt, np * nc);
+    if (lane < np) { S.pt[p0 + lane].sg = g; S.pt[p0 + lane].spad = pad; }
+  }
   __syncthreads();
-  for (int phase = 0; phase < 2; phase++) {
-    eval_walks<LDS, SPLIT>(S, P);
-    // argmax per point, with slow-path settling
+  // argmax per point of `mask` over its coarse (refine = false) or refine walks (first, count in
+  // Pt::pad), with slow-path settling; S.best[p] = the winning walk or PRIOR
+  auto settle = [&](unsigned mask, bool refine) {
     for (int round = 0; round < 2; round++) {
       if (wave == 0) {
         int slow = 0;
         for (int p = 0; p < np; p++) {
+          if (!((mask >> p) & 1u)) continue;  // uniform
           const Pt& pt = S.pt[p0 + p];
           int first, count;
           double pv;
-          if (phase == 0) { first = p * P.n_coarse; count = P.n_coarse; pv = -1.7976931348623157e308; }
+          if (!refine) { first = p * nc; count = nc; pv = -1.7976931348623157e308; }
           else { first = pt.pad >> 8; count = pt.pad & 0xFF; pv = pt.sm; }
           const int r = argmax_wave(S, first, count, pv, lane);
           if (r == AMBIG) slow = 1;
@@ -1279,47 +1347,54 @@ __device__ __forceinline__ void search_maxalpha_pts(Smem& S, const Params& P, in
       }
       __syncthreads();
     }
-    if (phase == 0) {
-      // record coarse winners (or the untouched initial state), lay out refine walks: wave 0,
-      // lane p for point p, then lane p * MAXREF + r for its refine walk r
-      if (wave == 0) {
-        int ci = 0, cnt = 0;
-        if (lane < np) {
-          const int bi = S.best[lane];
-          Pt& pt = S.pt[p0 + lane];
-          if (bi == PRIOR) { pt.la = LOG_AD_MAX; pt.sm = -1.7976931348623157e308; ci = P.n_coarse; }
-          else { pt.la = S.w[bi].la; pt.sm = S.val[bi]; ci = bi - lane * P.n_coarse; }
-          cnt = P.n_refine[ci];
-        }
-        int off = 0, nw = 0;
-        for (int p = 0; p < np; p++) {  // np <= 3, uniform
-          const int cp = __builtin_amdgcn_readlane(cnt, p);
-          if (lane == p) off = nw;
-          nw += cp;
-        }
-        if (lane < np) S.pt[p0 + lane].pad = (off << 8) | cnt;
-        if (lane == 0) { S.hkey = 1 + ci; S.nwalk = nw; }
-        const int p = lane / MAXREF, r = lane % MAXREF;
-        const int pc = p < np ? p : 0;
-        const int cip = __shfl(ci, pc, 64), cntp = __shfl(cnt, pc, 64), offp = __shfl(off, pc, 64);
-        if (p < np && r < cntp) {
-          Walk& V = S.w[offp + r];
-          V.p = p0 + p;
-          V.la = P.la_refine[cip * MAXREF + r];
-          V.dfail = P.dfail[P.n_coarse + cip * MAXREF + r];
-          V.len = 0; V.nl = V.nr = 0;
-        }
-      }
-      __syncthreads();
-    } else {
-      if (tid < np) {
-        Pt& pt = S.pt[p0 + tid];
-        const int bi = S.best[tid];
-        if (bi != PRIOR) { pt.la = S.w[bi].la; pt.sm = S.val[bi]; }
-        pt.clr = 2.0 * (pt.sm - pt.N);  // sm-search.c:298
-      }
-      __syncthreads();
+  };
+  // the refine argmax's result for the points of `mask` (sm-search.c:298 for every point)
+  auto finish = [&](unsigned mask) {
+    if (tid < np) {
+      Pt& pt = S.pt[p0 + tid];
+      const int bi = S.best[tid];
+      if (((mask >> tid) & 1u) && bi != PRIOR) { pt.la = S.w[bi].la; pt.sm = S.val[bi]; }
+      pt.clr = 2.0 * (pt.sm - pt.N);
     }
+    __syncthreads();
+  };
+  const unsigned all = (1u << np) - 1u;
+  eval_walks<LDS, SPLIT>(S, P);
+  settle(all, false);
+  // coarse winners (or the untouched initial state); the points whose guess held
+  if (wave == 0) {
+    bool hit = false;
+    if (lane < np) {
+      const int bi = S.best[lane];
+      Pt& pt = S.pt[p0 + lane];
+      int ci;
+      if (bi == PRIOR) { pt.la = LOG_AD_MAX; pt.sm = -1.7976931348623157e308; ci = nc; }
+      else { pt.la = S.w[bi].la; pt.sm = S.val[bi]; ci = bi - lane * nc; }
+      pt.ci = ci;
+      hit = spec && ci == pt.sg && P.spec_refine != 2;  // (FSCLG_SPEC_REFINE=2, tests: every guess taken as missed)
+      if (hit) pt.pad = pt.spad;
+    }
+    const unsigned hm = (unsigned)__ballot(hit) & all;
+    if (lane == 0) { S.hkey = 1 + S.pt[p0].ci; S.hitmask = (int)hm; }
+  }
+  __syncthreads();
+  const unsigned hm = (unsigned)__builtin_amdgcn_readfirstlane(S.hitmask);
+  if (hm) {  // refine argmax of the points whose speculative walks are the right ones
+    settle(hm, true);
+    finish(hm);
+  }
+  const unsigned miss = all & ~hm;
+  if (miss) {  // ---- refine phase for the rest
+    if (wave == 0) {
+      int ci = 0, cnt = 0;
+      if (lane < np && ((miss >> lane) & 1u)) { ci = S.pt[p0 + lane].ci; cnt = P.n_refine[ci]; }
+      const int pad = lay_refine(ci, cnt, 0);
+      if (lane < np && ((miss >> lane) & 1u)) S.pt[p0 + lane].pad = pad;
+    }
+    __syncthreads();
+    eval_walks<LDS, SPLIT>(S, P);
+    settle(miss, true);
+    finish(miss);
   }
 }
 
@@ -1336,8 +1411,8 @@ __device__ __forceinline__ void write_point(fsclg_point_t& o, const Pt& pt) {
   o.lalpha = pt.la; o.null_logl = pt.N; o.sm_logl = pt.sm; o.clr = pt.clr;
 }
 
-template <bool LDS, bool SPLIT>
-__device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
+template <bool LDS, bool SPLIT, class SM>
+__device__ __forceinline__ void maxpos_body(SM& S, const Params& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // cells arrive in the host's longest-first order (XCD-aware: blocks b and b + 8 share an
   // XCD); the hardware dispatches blocks in order (round-robin over the XCDs), so the long
@@ -1352,7 +1427,7 @@ __device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
     return;
   }
   if (tid < 8) S.cnt[tid] = 0;
-  if (tid < 4) S.tph[tid] = 0;
+  if (tid < 5) S.tph[tid] = 0;
   if (tid == 0) { S.cell = cell; S.member = member; S.inst = 0; S.xfail = 0; S.iev = 0; }
   if (P.ctrace && tid == 0 && member == 0) { P.ctrace[8 * cell] = wall_clock64(); P.ctrace[8 * cell + 2] = __smid(); }
   if constexpr (LDS) {
@@ -1373,7 +1448,8 @@ __device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
       pt.wend = in.window_end; pt.n_snps = in.n_snps; pt.flags = 0; pt.N = in.null_logl;
     }
     __syncthreads();
-    if (tid == 0) S.cnt[1] += (unsigned long long)S.pt[0].n_snps;
+    if (tid == 0) { S.cnt[1] += (unsigned long long)S.pt[0].n_snps; S.pt[0].sg = P.ci_guess; }
+    __syncthreads();
     search_maxalpha_pts<LDS, SPLIT>(S, P, 0, 1);  // split: the point's walks dealt over the members
     if (tid == 0 && member == 0) {
       S.pt[0].flags |= S.xfail;
@@ -1390,12 +1466,13 @@ __device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
   } else {
     const fsclg_cell_t c = P.cells[cell];
     if (P.cell_ep) {  // endpoints evaluated by a mode-2 launch (shared with the neighbouring cells)
-      if (tid < 2) read_point(S.pt[tid], P.ept[tid == 0 ? P.cell_ep[cell].x : P.cell_ep[cell].y]);
+      if (tid < 2) { read_point(S.pt[tid], P.ept[tid == 0 ? P.cell_ep[cell].x : P.cell_ep[cell].y]); S.pt[tid].ci = P.ci_guess; }
       __syncthreads();
     } else {
       if (wave < 2) init_point_wave(S.pt[wave], c.chr, wave == 0 ? c.start_pos : c.end_pos, P, lane);
       __syncthreads();
-      if (tid == 0) S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps);
+      if (tid == 0) { S.cnt[1] += (unsigned long long)(S.pt[0].n_snps + S.pt[1].n_snps); S.pt[0].sg = S.pt[1].sg = P.ci_guess; }
+      __syncthreads();
       search_maxalpha_pts<LDS, SPLIT>(S, P, 0, 2);  // start and end points share the two phases
     }
     // the bisection (scan-chromosome.c:103-139), two levels per alpha search: a level goes
@@ -1430,6 +1507,10 @@ __device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
         }
         __syncthreads();
       }
+      // split cells' speculative refine walks: the better end's coarse winner (the bisection
+      // heads towards it, and a point's winner changes slowly along the chromosome)
+      if (tid == 0) S.pt[2].sg = S.pt[3].sg = S.pt[0].clr >= S.pt[1].clr ? S.pt[0].ci : S.pt[1].ci;
+      __syncthreads();
       search_maxalpha_pts<LDS, SPLIT>(S, P, 2, two ? 2 : 1);
       // every thread takes the same decisions from the same shared values (uniform control)
       const bool left = (S.pt[0].clr + S.pt[2].clr) >= (S.pt[1].clr + S.pt[2].clr);
@@ -1463,6 +1544,9 @@ __device__ __forceinline__ void maxpos_body(Smem& S, const Params& P) {
   if (P.ctrace && tid == 0) {
     P.ctrace[8 * cell + 1] = wall_clock64(); P.ctrace[8 * cell + 3] = S.cnt[0];
     for (int k = 0; k < 4; k++) P.ctrace[8 * cell + 4 + k] = S.tph[k];
+#ifdef FSCLG_PHASE_TIMING
+    P.ctrace[8 * cell + 2] = S.tph[4] | ((unsigned long long)S.inst << 48);  // (the CU id's slot; + the phases)
+#endif
   }
 }
 
@@ -1482,7 +1566,7 @@ search_maxpos_kernel(Params P) {
 template <bool LDS>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(FSCLG_WPE_SPLIT, FSCLG_WPE_SPLIT)))
 search_maxpos_split_kernel(Params P) {
-  __shared__ Smem S;
+  __shared__ SmemSplit S;
   maxpos_body<LDS, true>(S, P);
 }
 
@@ -1862,6 +1946,8 @@ struct fsclg_ctx {
   std::unordered_map<unsigned long long, uint32_t> cell_cost;  // (chr, start, end) -> cost of its last run
   unsigned long long n_dup_cells = 0, n_ep_saved = 0;
   unsigned long long n_split_retry = 0;
+  unsigned long long ci_count[16] = {0};  // results' coarse alpha index (nearest coarse grid value): the guess
+  int ci_guess = 5;                       // of split cells' speculative refine walks (Params::ci_guess)
   double kernel_ms = 0.0;
   unsigned long long launches = 0;
   std::vector<std::pair<double, double>> busy;  // [start, end) ms of each batch's kernels since ev_ref
@@ -2631,6 +2717,7 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
   P.split = 1; P.xacc = nullptr; P.xcnt = nullptr;
+  P.spec_refine = 0; P.ci_guess = std::min(c->ci_guess, c->n_coarse);
   static const int lookahead = getenv("FSCLG_LOOKAHEAD") ? atoi(getenv("FSCLG_LOOKAHEAD")) : 1;
   P.lookahead = lookahead;
   if (getenv("FSCLG_CELL_TRACE")) {
@@ -2647,20 +2734,40 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   return P;
 }
 
+// split cells' speculative refine walks (FSCLG_SPEC_REFINE=0: off, for A/B runs and tests; 2: evaluated
+// but every guess taken as missed, the fallback path's test)
+static int spec_refine_on() {
+  static const int on = getenv("FSCLG_SPEC_REFINE") ? atoi(getenv("FSCLG_SPEC_REFINE")) : 1;
+  return on;
+}
+
+// the guess for points with no evaluated neighbour: the most frequent coarse alpha index among
+// the results so far (a point's lalpha lies within one coarse step of its coarse winner)
+static void note_alphas(fsclg_ctx* c, const fsclg_point_t* out, int n) {
+  const int nc = std::min(c->n_coarse, 15);
+  for (int i = 0; i < n; i++) {
+    const double k = floor((out[i].lalpha - LOG_AD_MIN) / 2.4 + 0.5);
+    if (k >= 0.0 && k <= (double)nc) c->ci_count[(int)k]++;
+  }
+  int best = c->ci_guess;
+  for (int k = 0; k <= nc; k++) if (c->ci_count[k] > c->ci_count[best]) best = k;
+  c->ci_guess = best;
+}
+
 // one launch of search_maxpos_kernel with n blocks on the batch's stream (events recorded by the caller)
 static int launch_blocks(hipStream_t stream, const Params& P, int n) {
   const int grid = n;
   const int dyn = P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
-  const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
-  if (stat + dyn <= LDS_WG) {
+  const int stat_m = (int)((sizeof(Smem) + 15) / 16 * 16), stat_s = (int)((sizeof(SmemSplit) + 15) / 16 * 16);
+  if ((P.split > 1 ? stat_s : stat_m) + dyn <= LDS_WG) {
     static unsigned long long attr_set = 0;  // per device (bit = device id)
     int dev = 0;
     HIPCHK(hipGetDevice(&dev), "hipGetDevice");
     if (dev >= 64 || !(attr_set >> dev & 1ull)) {
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat_m), "hipFuncSetAttribute");
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_split_kernel<true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat), "hipFuncSetAttribute");
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat_s), "hipFuncSetAttribute");
       if (dev < 64) attr_set |= 1ull << dev;
     }
     if (P.split > 1) hipLaunchKernelGGL((search_maxpos_split_kernel<true>), dim3(grid), dim3(WG), dyn, stream, P);
@@ -2893,6 +3000,7 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
     HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");  // the exchange
                                                                                                   // areas need no zeroing
     P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
+    P.spec_refine = spec_refine_on();
     // latency: no LDS coefficient windows (their loads, repeated by every member for every
     // phase, cost more than the global gathers of a lightly loaded device)
     P.ivc0 = 0; P.n_civ = 0; P.civ_max = 0; P.n_cache = 0;
@@ -2982,6 +3090,7 @@ int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
     if (r) return r;
     return fsclg_search_wait(c, batch, out);
   }
+  note_alphas(c, out, B.n_cells);
   for (int i = 0; i < B.n_cells; i++)
     if (out[i].flags)
       return set_err(out[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL,
@@ -3043,6 +3152,7 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
     if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, nl))) return r;
     HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");
     P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
+    P.spec_refine = spec_refine_on();
     P.ivc0 = 0; P.n_civ = 0; P.civ_max = 0; P.n_cache = 0;  // as a split batch: no LDS coefficient windows
     P.off_thr = 0; P.off_nul = (c->n_iv + 1) * 8;
     P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8;
@@ -3052,6 +3162,7 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
   HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
   HIPCHK(hipEventSynchronize(B.ev1), "hipEventSynchronize");
   memcpy(pts, B.p_out, sizeof(fsclg_point_t) * n_pts);
+  note_alphas(c, pts, n_pts);
   for (int i = 0; i < n_pts; i++)
     if (pts[i].flags & (PF_UNSUPPORTED | PF_SPLIT_TIMEOUT))
       return set_err(pts[i].flags & PF_UNSUPPORTED ? FSCLG_E_UNSUPPORTED : FSCLG_E_KERNEL,

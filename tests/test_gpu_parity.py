@@ -71,6 +71,30 @@ def test_bisection_lookahead_fallbacks(built, tmp, lookahead):
         assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text(), case
 
 
+@pytest.mark.parametrize("spec", ["0", "2"])
+def test_speculative_refine_fallbacks(built, tmp, spec):
+    """Split cells evaluate the refine walks of a guessed coarse winner beside the coarse walks
+    (on by default, so every other test runs it).  Off, and evaluated but every
+    guess taken as missed (each point then takes the second phase): the golden outputs either
+    way, and the oracle's on a multi-chromosome permutation job."""
+    env = dict(os.environ, FSCLG_SPEC_REFINE=spec)
+    for case in ("g1_p25", "g1_asc", "g3_p10"):
+        c = manifest()["cases"][case]
+        r = subprocess.run([str(CLI), "-f", str(GOLD / c["input"]), "-o", str(tmp / "o.txt"), *c["options"]],
+                           capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, r.stderr
+        assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text(), case
+    snp = tmp / "m.snp"
+    synth.write_snp_file(str(snp), synth.generate(n_chr=3, chr_len=3_000_000, snps_per_chr=3000, n=30, seed=71,
+                                                  sweeps_per_chr=1))
+    opts = ["--n-permute=40"]
+    run_oracle(snp, tmp / "r.txt", opts)
+    r = subprocess.run([str(CLI), "-f", str(snp), "-o", str(tmp / "g.txt"), *opts], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stderr
+    assert (tmp / "g.txt").read_text() == (tmp / "r.txt").read_text()
+
+
 @pytest.mark.parametrize("case", ["g1_p25", "g2_grid50k", "g3_scan"])
 def test_cli_matches_golden(built, tmp, case):
     c = manifest()["cases"][case]

@@ -3,7 +3,7 @@
 set -o pipefail
 TAG=$1
 R=${GRAFT_REPO_ROOT:-$PWD}
-export FSCL_AMD_LIBDIR=$R/fscl_amd/_build_rehearsal
+export FSCL_AMD_LIBDIR=$R/fscl_amd/_build_${VARIANT:-rehearsal}
 OUT=$R/gpurun_out/tail_$TAG
 mkdir -p $OUT
 REC=/tmp/fscl_sim_$TAG.bin
