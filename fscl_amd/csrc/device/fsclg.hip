@@ -21,7 +21,9 @@
 //
 // Few-cell launches (the permutation pipeline's blocking batches, the drop-in search_maxalpha)
 // give each cell up to 8 workgroups ("split cells") that share the walks' segments and combine
-// their sums through per-cell agent-scope exchange areas.
+// their sums through per-cell agent-scope exchange areas.  A split cell's
+// alpha search also evaluates the refine walks of a guessed coarse winner beside the coarse
+// walks, so that a correct guess saves the refine phase (SmemSplit: 64 walk slots; §10.6).
 //
 // Arithmetic is compiled with contraction off (no FMA fusing): the reference's polynomial and
 // log(alpha d) adds are reproduced operation for operation.
