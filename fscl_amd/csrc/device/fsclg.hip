@@ -1850,7 +1850,6 @@ struct Slot {
   int wtask_cap = 0;
   uint32_t* h_rows = nullptr;     // pinned (coherent) staging of one trial's rows, read by scatter_rows_kernel
   double* h_null = nullptr;       // pinned (coherent) whole-chromosome null sums, n_chr
-  uint32_t* d_stage = nullptr;    // FSCLG_UPLOAD_COPY: device copy of a trial's packed rows (copy engine)
   int rows_cap = 0, null_cap = 0;
   hipEvent_t ready = nullptr;     // recorded on the upload stream after the slot's last upload
   hipEvent_t wev0 = nullptr, wev1 = nullptr;  // bracket the slot's last window null-sum launch
@@ -2065,8 +2064,7 @@ int fsclg_close(fsclg_ctx* c) {
                   c->d_stats, c->d_dfail};
   for (void* p : ptrs) if (p) hipFree(p);
   for (Slot& S : c->slot) {
-    for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null, (void*)S.d_ctab, (void*)S.d_stage})
-      if (p) hipFree(p);
+    for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null, (void*)S.d_ctab}) if (p) hipFree(p);
     for (void* p : {(void*)S.h_rows, (void*)S.h_null, (void*)S.p_wtasks}) if (p) hipHostFree(p);
     hipEventDestroy(S.ready);
     if (S.wev0) hipEventDestroy(S.wev0);
@@ -2293,17 +2291,8 @@ int fsclg_slot_set_rows_packed(fsclg_ctx* c, int slot, const void* row, int row_
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read h_null
   S.win_valid = false; S.ctab_valid = false;
   if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
-  // read straight from the caller's portable pinned rows (one buffer can feed every device);
-  // FSCLG_UPLOAD_COPY=1 (experiment): one copy-engine transfer of the packed rows into device
-  // staging on the upload stream first, the scatter then reads device memory
+  // read straight from the caller's portable pinned rows (one buffer can feed every device)
   const double* cn = chr_null ? S.h_null : nullptr;
-  static const bool ucopy = getenv("FSCLG_UPLOAD_COPY") && atoi(getenv("FSCLG_UPLOAD_COPY")) > 0;
-  if (ucopy) {
-    if (!S.d_stage) HIPCHK(hipMalloc((void**)&S.d_stage, sizeof(uint32_t) * ((size_t)c->n_snps + 64)), "hipMalloc row staging");
-    HIPCHK(hipMemcpyAsync(S.d_stage, row, (size_t)c->n_snps * row_bytes, hipMemcpyHostToDevice, c->ustream),
-           "hipMemcpyAsync rows");
-    row = S.d_stage;
-  }
   const int per = 256 * (16 / row_bytes);  // sites per block
   const dim3 grid((c->n_snps + per - 1) / per);
   if (row_bytes == 1)
