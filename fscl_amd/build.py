@@ -65,7 +65,8 @@ def build_native(force: bool = False, trace: bool = False, variant: str | None =
 
 def _build_native(force: bool, trace: bool, defines: tuple[str, ...] = ()) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
-    hdrs = list((ROOT / "include").glob("*.h")) + [CSRC / "host" / "fscl_host.h"] + [Path(__file__)]  # flags live here
+    # every header a source may include (csrc/host/*.h: fscl_host.h, rows_impl.h, ...) and this file (the flags)
+    hdrs = list((ROOT / "include").glob("*.h")) + sorted((CSRC / "host").glob("*.h")) + [Path(__file__)]
     objs = []
     for src in HOST_SRC:
         s = CSRC / "host" / src

@@ -107,6 +107,7 @@ static_assert(U_MAIN % 2 == 0 && U_SPLIT % 2 == 0, "the interleaved site array h
 __host__ __device__ __forceinline__ uint32_t phys(uint32_t i) { return (i & ~127u) | ((i & 63u) << 1) | ((i >> 6) & 1u); }
 
 enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2, PF_SPLIT_TIMEOUT = 4 };
+constexpr unsigned int XFAIL_BIT = 0x80000000u;  // split cells: a member's timeout, in the cell's arrival word
 
 struct Params {
   const uint2* pr;             // [n_snps + PAD] (position ^ POS_BIAS, device row = caller's row + 1; 0: zero sentinel)
@@ -162,7 +163,10 @@ struct Params {
                                // coarse walks (one phase per alpha search when the guess holds)
   int ci_guess;                // the guess for points with no evaluated neighbour (the recent results' mode)
   char* xacc;                  // [n_cells][2] XAcc
-  unsigned int* xcnt;          // [n_cells] arrivals
+  unsigned int* xcnt;          // [n_cells] arrivals; bit 31: some member of the cell timed out (XFAIL_BIT)
+  unsigned long long xwait;    // split cells: wall-clock ticks (100 MHz) a member waits for the others
+  unsigned long long xdelay;   // tests only (FSCLG_TEST_SPLIT_DELAY_US): member 0 of cell 0 sleeps this
+                               // long before its first arrival, so that the other members time out
 };
 
 struct Pt {                     // one scan point being evaluated (scan_pt_t subset)
@@ -1009,13 +1013,28 @@ __device__ __forceinline__ void combine_members(SM& S, const Params& P, int nw) 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned int* cnt = P.xcnt + S.cell;
+    if (P.xdelay && inst == 0 && me == 0 && S.cell == 0) {  // tests: a member that is late by more than the wait
+      const unsigned long long td = wall_clock64();
+      while (wall_clock64() - td < P.xdelay) __builtin_amdgcn_s_sleep(127);
+    }
     ag_add32(cnt, 1u);
     const unsigned int target = (unsigned)G * (unsigned)(inst + 1);
     const unsigned long long t0 = wall_clock64();
-    while (ag_add32(cnt, 0u) < target) {
+    unsigned int v;
+    while (((v = ag_add32(cnt, 0u)) & ~XFAIL_BIT) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > 100000000ull) { S.xfail = PF_SPLIT_TIMEOUT; break; }  // ~1 s at 100 MHz
+      if (wall_clock64() - t0 > P.xwait) {  // a member never arrived: publish it for the whole cell
+        S.xfail = PF_SPLIT_TIMEOUT;
+        ag_or32(cnt, XFAIL_BIT);
+        break;
+      }
     }
+    // Another member timed out (it went on with partial sums and may have overwritten this
+    // instance's region), or more arrivals than members one instance ahead can make: either way
+    // this cell's sums are not the reference's, and member 0 flags its point for the unsplit
+    // re-run.  A member's flag precedes its later arrivals in the counter's order, so any
+    // arrival a waiting member counted carries the flag of a timeout before it.
+    if ((v & XFAIL_BIT) || (v & ~XFAIL_BIT) >= target + (unsigned)G) S.xfail = PF_SPLIT_TIMEOUT;
 #ifdef FSCLG_PHASE_TIMING
     S.tph[4] += wall_clock64() - t0;
 #endif
@@ -2263,6 +2282,25 @@ void fsclg_host_free(void* p) {
   if (p) hipHostFree(p);
 }
 
+int fsclg_host_register(void* p, size_t bytes) {
+  if (!p || !bytes) return set_err(FSCLG_E_ARG, "host register");
+  hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterMapped);
+  if (e != hipSuccess) return set_err(FSCLG_E_HIP, "hipHostRegister", e);
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, p, 0);
+  if (e != hipSuccess || d != p) {  // the kernels take the host pointer as it is
+    hipHostUnregister(p);
+    return set_err(e != hipSuccess ? FSCLG_E_HIP : FSCLG_E_STATE, "hipHostGetDevicePointer", e);
+  }
+  return FSCLG_OK;
+}
+
+int fsclg_host_unregister(void* p) {
+  if (!p) return FSCLG_OK;
+  const hipError_t e = hipHostUnregister(p);
+  return e == hipSuccess ? FSCLG_OK : set_err(FSCLG_E_HIP, "hipHostUnregister", e);
+}
+
 int fsclg_slot_wait(fsclg_ctx* c, int slot) {
   if (!c) return set_err(FSCLG_E_ARG, "ctx");
   if (slot < 0 || slot >= NSLOT) return set_err(FSCLG_E_ARG, "slot");
@@ -2719,6 +2757,14 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
   P.split = 1; P.xacc = nullptr; P.xcnt = nullptr;
+  {
+    const unsigned long long wait_us =
+        getenv("FSCLG_SPLIT_WAIT_US") ? strtoull(getenv("FSCLG_SPLIT_WAIT_US"), nullptr, 10) : 1000000ull;
+    const unsigned long long delay_us =
+        getenv("FSCLG_TEST_SPLIT_DELAY_US") ? strtoull(getenv("FSCLG_TEST_SPLIT_DELAY_US"), nullptr, 10) : 0ull;
+    P.xwait = wait_us * 100ull;  // wall_clock64 runs at 100 MHz
+    P.xdelay = delay_us * 100ull;
+  }
   P.spec_refine = 0; P.ci_guess = std::min(c->ci_guess, c->n_coarse);
   static const int lookahead = getenv("FSCLG_LOOKAHEAD") ? atoi(getenv("FSCLG_LOOKAHEAD")) : 1;
   P.lookahead = lookahead;

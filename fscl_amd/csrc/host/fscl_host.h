@@ -59,6 +59,20 @@ void fh_shm_close(fh_shm_t *m);
 int fh_shm_allgather(fh_shm_t *m, void *buf, size_t item, int n, int lo, int hi);
 int fh_shm_allgather_flags(fh_shm_t *m, void *buf, size_t item, int n, int lo, int hi, unsigned *flags);
 int fh_shm_barrier(fh_shm_t *m);
+int fh_shm_rank(const fh_shm_t *m);
+int fh_shm_world(const fh_shm_t *m);
+
+/* the node leader's permutation pool: a second shared segment holding every trial's rows,
+   built once by rank 0 and read by every rank's devices (ranks.c) */
+typedef struct fh_pool fh_pool_t;
+fh_pool_t *fh_pool_open(fh_shm_t *m, size_t data_bytes);  /* collective */
+void fh_pool_close(fh_pool_t *p);
+char *fh_pool_data(fh_pool_t *p);
+size_t fh_pool_bytes(const fh_pool_t *p);
+int fh_pool_publish(fh_pool_t *p, size_t rows_off, size_t nul_off, const fh_rand_t *end, unsigned long long negj);
+int fh_pool_take(fh_pool_t *p, size_t *rows_off, size_t *nul_off, fh_rand_t *end, unsigned long long *negj);
+void fh_pool_release(fh_pool_t *p);
+int fh_pool_wait_released(fh_pool_t *p);
 
 /* ms reader */
 scan_t *fh_load_ms(const char *fname, int segment_length, int folded, int sample_first, int sample_size);

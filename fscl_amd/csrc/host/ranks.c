@@ -62,6 +62,8 @@ struct fh_shm {
   size_t map_bytes;
   unsigned long long seq;  /* exchanges done by this rank */
   int rank, world;
+  char name[200];          /* the segment's name: the permutation pools' names derive from it */
+  unsigned n_pools;        /* pools opened so far (the same count on every rank: collective) */
 };
 
 static double timeout_s(void) {
@@ -102,6 +104,7 @@ fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap) {
   }
   m = fh_calloc(1, sizeof *m, "shm");
   m->rank = rank; m->world = world; m->map_bytes = bytes;
+  snprintf(m->name, sizeof m->name, "%s", name);
   if (rank == 0) {
     fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd < 0) {
@@ -206,4 +209,131 @@ int fh_shm_allgather(fh_shm_t *m, void *buf, size_t item, int n, int lo, int hi)
 int fh_shm_barrier(fh_shm_t *m) {
   char dummy = 0;
   return fh_shm_allgather_flags(m, &dummy, 1, 0, 0, 0, NULL);
+}
+
+int fh_shm_rank(const fh_shm_t *m) { return m->rank; }
+int fh_shm_world(const fh_shm_t *m) { return m->world; }
+
+/* ------------------------------------------------------------------ permutation pool
+   One node leader (rank 0) builds each trial's block permutation once (scan-chromosome.c:
+   441-456: the serial permutation at the trial barrier), with speculation over the whole
+   node's spare CPUs, straight into buffers of a second shared-memory segment that every rank
+   maps (and page-locks, so that its devices' scatter kernels read the rows from it directly).
+   Per trial the leader publishes (rows offset, null-sums offset, rand() state after the
+   permutation, negative-j count) in a ring; every other rank takes the publications in order,
+   continues the rand() stream from the published state (the prune draws that follow are the
+   same on every rank: same results, same order) and uploads the leader's rows.  A buffer is
+   reused only after every rank has released the row slot that read it (per-rank release
+   counters), and a ring entry only after every rank has taken it. */
+#define POOL_RING 32
+#define POOL_HDR (64u << 10)
+
+typedef struct {
+  unsigned long long seq;          /* 1-based publication number */
+  unsigned long long rows_off, nul_off, negj;
+  fh_rand_t end;                   /* the stream after this permutation */
+} pool_pub_t;
+
+typedef struct {
+  _Atomic unsigned long long pub;                 /* publications so far */
+  _Atomic unsigned long long cons[SHM_MAX_RANKS]; /* publications taken, per rank */
+  _Atomic unsigned long long rel[SHM_MAX_RANKS];  /* row-slot releases, per rank */
+  unsigned long long data_bytes;
+  pool_pub_t ring[POOL_RING];
+} pool_hdr_t;
+
+_Static_assert(sizeof(pool_hdr_t) <= POOL_HDR, "pool header");
+
+struct fh_pool {
+  fh_shm_t *m;
+  pool_hdr_t *h;
+  char *data;
+  size_t map_bytes, data_bytes;
+  unsigned long long n_pub, n_take, n_rel;  /* this rank's counts */
+};
+
+/* collective (every rank of m, in the same order of calls): rank 0 creates a segment of
+   data_bytes (the others' argument is ignored: they map what rank 0 made) */
+fh_pool_t *fh_pool_open(fh_shm_t *m, size_t data_bytes) {
+  char name[256];
+  fh_pool_t *p = fh_calloc(1, sizeof *p, "pool");
+  int fd = -1;
+  p->m = m;
+  snprintf(name, sizeof name, "%s_pool%u", m->name, m->n_pools++);
+  if (m->rank == 0) {
+    p->data_bytes = (data_bytes + 4095) & ~(size_t)4095;
+    p->map_bytes = POOL_HDR + p->data_bytes;
+    fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0 || ftruncate(fd, (off_t)p->map_bytes) != 0)
+      logmsg(MSG_FATAL, "fscl_amd: permutation pool %s: %s", name, strerror(errno));
+  }
+  if (fh_shm_barrier(m) != 0) logmsg(MSG_FATAL, "fscl_amd: permutation pool: rank exchange failed");
+  if (m->rank != 0) {
+    struct stat sb;
+    fd = shm_open(name, O_RDWR, 0600);
+    if (fd < 0 || fstat(fd, &sb) != 0 || (size_t)sb.st_size <= POOL_HDR)
+      logmsg(MSG_FATAL, "fscl_amd: permutation pool %s: %s", name, strerror(errno));
+    p->map_bytes = (size_t)sb.st_size;
+    p->data_bytes = p->map_bytes - POOL_HDR;
+  }
+  p->h = mmap(NULL, p->map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p->h == MAP_FAILED) logmsg(MSG_FATAL, "fscl_amd: permutation pool mmap: %s", strerror(errno));
+  p->data = (char *)p->h + POOL_HDR;
+  if (fh_shm_barrier(m) != 0) logmsg(MSG_FATAL, "fscl_amd: permutation pool: rank exchange failed");
+  if (m->rank == 0) shm_unlink(name);  /* every rank has it mapped */
+  return p;
+}
+
+void fh_pool_close(fh_pool_t *p) {
+  if (!p) return;
+  munmap(p->h, p->map_bytes);
+  free(p);
+}
+
+char *fh_pool_data(fh_pool_t *p) { return p->data; }
+size_t fh_pool_bytes(const fh_pool_t *p) { return p->data_bytes; }
+
+/* the leader: publish one trial's permutation (offsets into the data area) */
+int fh_pool_publish(fh_pool_t *p, size_t rows_off, size_t nul_off, const fh_rand_t *end, unsigned long long negj) {
+  const unsigned long long s = p->n_pub + 1;
+  pool_pub_t *e = &p->h->ring[(s - 1) % POOL_RING];
+  int r;
+  if (s > POOL_RING)  /* the entry's previous publication taken by every rank */
+    for (r = 1; r < p->m->world; r++)
+      if (wait_ge_ull(&p->h->cons[r], s - POOL_RING) != 0) return -1;
+  e->rows_off = rows_off; e->nul_off = nul_off; e->negj = negj; e->end = *end; e->seq = s;
+  atomic_store_explicit(&p->h->pub, s, memory_order_release);
+  p->n_pub = s;
+  return 0;
+}
+
+/* the other ranks: the next publication, in order */
+int fh_pool_take(fh_pool_t *p, size_t *rows_off, size_t *nul_off, fh_rand_t *end, unsigned long long *negj) {
+  const unsigned long long s = p->n_take + 1;
+  const pool_pub_t *e = &p->h->ring[(s - 1) % POOL_RING];
+  if (wait_ge_ull(&p->h->pub, s) != 0) return -1;
+  if (e->seq != s) {
+    logmsg(MSG_ERROR, "fscl_amd: permutation pool: publication %llu found, %llu expected", e->seq, s);
+    return -1;
+  }
+  *rows_off = e->rows_off; *nul_off = e->nul_off; *end = e->end; *negj = e->negj;
+  atomic_store_explicit(&p->h->cons[p->m->rank], s, memory_order_release);
+  p->n_take = s;
+  return 0;
+}
+
+/* this rank's devices have finished reading one more row slot */
+void fh_pool_release(fh_pool_t *p) {
+  p->n_rel++;
+  atomic_store_explicit(&p->h->rel[p->m->rank], p->n_rel, memory_order_release);
+}
+
+/* the leader: every rank has made as many releases as this one (their uploads of the
+   released slots' rows are done: the buffers may be rewritten) */
+int fh_pool_wait_released(fh_pool_t *p) {
+  int r;
+  for (r = 0; r < p->m->world; r++)
+    if (r != p->m->rank && wait_ge_ull(&p->h->rel[r], p->n_rel) != 0) return -1;
+  return 0;
 }

@@ -179,8 +179,11 @@ int fscl_amd_set_device(int device) { return fscl_amd_set_devices(&device, 1); }
 
 int fscl_amd_n_devices(void) { return D.n_dev; }
 
+static void pool_drop(void);
+
 int fscl_amd_set_ranks(int rank, int world, fscl_amd_exchange_fn fn, void *ctx) {
   if (world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return -1;
+  pool_drop();  /* the pool belongs to the old exchange */
   fh_shm_close(D.shm); D.shm = NULL;
   D.rank = rank; D.world = world; D.xfn = fn; D.xctx = ctx;
   return 0;
@@ -190,6 +193,7 @@ int fscl_amd_set_ranks_shm(int rank, int world, const char *name) {
   const char *e = getenv("FSCL_AMD_SHM_MB");
   const size_t cap = (size_t)(e && atoi(e) > 0 ? atoi(e) : 64) << 20;
   if (world < 1 || rank < 0 || rank >= world || !name) return -1;
+  pool_drop();  /* the pool belongs to the old exchange */
   fh_shm_close(D.shm); D.shm = NULL;
   D.rank = rank; D.world = world; D.xfn = NULL; D.xctx = NULL;
   if (world == 1) return 0;
@@ -543,22 +547,32 @@ static void dev_shares(const double *cost, int n, int *lo, int *hi) {
   }
 }
 
-/* complete a batch's results on every rank: this process holds [lo, hi) of out[n] */
-static void exchange_points(fsclg_point_t *out, int n, int lo, int hi) {
+/* complete a batch's results on every rank: this process holds [lo, hi) of out[n].  With
+   `flags` (this rank's flag word on entry, the OR over the ranks on return) the exchange is
+   made even for an empty batch, and out[] must have room for n + 1 items (the torch
+   exchange carries the word in item n). */
+static void exchange_points_flags(fsclg_point_t *out, int n, int lo, int hi, unsigned *flags) {
 #ifdef FSCL_AMD_REHEARSAL
   if (D.sim) { sim_exchange(out, n, lo, hi); return; }
 #endif
-  if (D.world <= 1 || n == 0) return;
+  if (D.world <= 1 || (n == 0 && !flags)) return;
   if (D.shm) {
-    if (fh_shm_allgather(D.shm, out, sizeof(fsclg_point_t), n, lo, hi) != 0)
+    if (fh_shm_allgather_flags(D.shm, out, sizeof(fsclg_point_t), n, lo, hi, flags) != 0)
       logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
     return;
   }
   memset(out, 0, sizeof(fsclg_point_t) * (size_t)lo);
   memset(out + hi, 0, sizeof(fsclg_point_t) * (size_t)(n - hi));
-  if (D.xfn((long long *)out, (int)(n * (sizeof(fsclg_point_t) / sizeof(long long))), D.xctx) != 0)
+  if (flags) {
+    memset(out + n, 0, sizeof(fsclg_point_t));
+    ((long long *)(out + n))[0] = *flags;
+  }
+  if (D.xfn((long long *)out, (int)((n + (flags ? 1 : 0)) * (sizeof(fsclg_point_t) / sizeof(long long))), D.xctx) != 0)
     logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
+  if (flags) *flags = ((long long *)(out + n))[0] != 0;
 }
+
+static void exchange_points(fsclg_point_t *out, int n, int lo, int hi) { exchange_points_flags(out, n, lo, hi, NULL); }
 
 /* the cost of a cell: its window size (snp_likelihood terms scale with it) */
 static double window_cost(int chr, int eval_range) {
@@ -768,6 +782,7 @@ static struct {
   double nbp, width_mb;
   pbuf_t pb[FSCLG_N_SLOTS + 2 * SPEC_MAX + 1];
   int n_pb, pb_cap, pb_nchr, pb_rb;
+  int pb_in_pool;         /* the buffers are the leader's pool's (not owned here) */
 } SP = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
 
 static void *spec_worker(void *arg) {
@@ -827,11 +842,31 @@ static int usable_cpus(void) {
   return n;
 }
 
+/* The node leader's permutations (one process per GPU, parity mode): rank 0 builds every
+   trial's permutation once, with speculation on the node's spare CPUs, into a shared pool
+   that every rank's devices read (ranks.c, fh_pool_*); the other ranks take each trial's
+   rows and rand() state from it instead of replaying the permutation and its speculation.
+   FSCL_AMD_PERM_LEADER=0 turns it off (every rank builds its own, as before). */
+static struct {
+  int on;            /* in the current permute_pipelined call */
+  fh_pool_t *pool;
+  int registered;    /* this rank's devices read the pool directly (else: a copy into D.stage) */
+} PL;
+
+static int perm_leader_wanted(void) {
+  const char *e = getenv("FSCL_AMD_PERM_LEADER");
+  return D.world > 1 && D.shm && !D.sim && (!e || atoi(e) != 0);
+}
+
 /* worker threads: FSCL_AMD_SPEC, else this process's share of the usable CPUs (one process
-   per GPU shares the node: LOCAL_WORLD_SIZE) less the main thread */
+   per GPU shares the node: LOCAL_WORLD_SIZE) less the main thread.  With the node leader's
+   permutations: the leader takes every CPU the ranks' main threads leave, the others none */
 static int spec_threads_wanted(void) {
   const char *e = getenv("FSCL_AMD_SPEC"), *lw = getenv("LOCAL_WORLD_SIZE");
-  int n = e ? atoi(e) : usable_cpus() / (lw && atoi(lw) > 0 ? atoi(lw) : 1) - 1;
+  const int local = lw && atoi(lw) > 0 ? atoi(lw) : PL.on ? D.world : 1;
+  int n;
+  if (PL.on && D.rank != 0) return 0;
+  n = e ? atoi(e) : PL.on ? usable_cpus() - local : usable_cpus() / local - 1;
   return n < 0 ? 0 : n > SPEC_MAX ? SPEC_MAX : n;
 }
 
@@ -853,14 +888,16 @@ static void spec_stop(void) {
   for (t = 0; t < SP.n_th; t++) pthread_join(SP.th[t], NULL);
   SP.n_th = 0;
   SP.stop = 0;
-  for (t = 0; t < SP.n_pb; t++) { fsclg_host_free(SP.pb[t].buf); free(SP.pb[t].nul); }
-  SP.n_pb = SP.pb_cap = SP.pb_nchr = SP.pb_rb = 0;
+  if (!SP.pb_in_pool)
+    for (t = 0; t < SP.n_pb; t++) { fsclg_host_free(SP.pb[t].buf); free(SP.pb[t].nul); }
+  SP.n_pb = SP.pb_cap = SP.pb_nchr = SP.pb_rb = SP.pb_in_pool = 0;
 }
 
 /* buffers for K slots, the candidates and the main thread's own (no job posted) */
 static void pb_reserve(int n_snps, int K) {
   const int want = K + 2 * SP.n_th + 1;
   int b;
+  if (SP.pb_in_pool) { SP.n_pb = 0; SP.pb_in_pool = 0; SP.pb_cap = 0; }
   if (SP.pb_cap < n_snps || SP.pb_nchr < D.n_chr || SP.pb_rb != D.rb) {
     for (b = 0; b < SP.n_pb; b++) { fsclg_host_free(SP.pb[b].buf); free(SP.pb[b].nul); }
     SP.n_pb = 0;
@@ -885,11 +922,63 @@ static int pb_get(void) {
   return -1;
 }
 
-/* the slot's last upload has read its buffer on every local device: free it */
+/* the slot's last upload has read its buffer on every local device: free it (the leader's
+   pool: once every rank has released the slot too; the releases are counted per rank, and
+   every rank makes the same sequence of them) */
 static void slot_release(int slot) {
   int l, b;
   for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_wait(D.ctx[l], slot), "slot wait");
+  if (PL.on) {
+    fh_pool_release(PL.pool);
+    if (D.rank == 0 && fh_pool_wait_released(PL.pool) != 0)
+      logmsg(MSG_FATAL, "fscl_amd: permutation pool: a rank stopped releasing its row slots");
+  }
   for (b = 0; b < SP.n_pb; b++) if (SP.pb[b].owner == slot) SP.pb[b].owner = PB_FREE;
+}
+
+/* collective: a pool large enough for the leader's buffers (K slots, two per worker thread, one
+   for the main thread), then (leader) the buffers carved from it */
+static void pool_setup(int n_snps, int K) {
+  const size_t rows = ((size_t)D.rb * (size_t)(n_snps ? n_snps : 1) + 4095) & ~(size_t)4095;
+  const size_t nulb = ((sizeof(double) * (size_t)(D.n_chr ? D.n_chr : 1)) + 255) & ~(size_t)255;
+  const int nbuf = K + 2 * SP.n_th + 1;
+  const size_t want = (size_t)nbuf * (rows + nulb);
+  unsigned f = D.rank == 0 && (!PL.pool || fh_pool_bytes(PL.pool) < want) ? 1u : 0u;
+  char dummy = 0;
+  int b;
+  if (fh_shm_allgather_flags(D.shm, &dummy, 1, 0, 0, 0, &f) != 0) logmsg(MSG_FATAL, "fscl_amd: rank exchange failed");
+  if (f) {  /* the leader needs a new pool: every rank drops the old one and maps the new one */
+    if (PL.pool) {
+      if (PL.registered) fsclg_host_unregister(fh_pool_data(PL.pool));
+      fh_pool_close(PL.pool);
+    }
+    PL.pool = fh_pool_open(D.shm, want);
+    PL.registered = fsclg_host_register(fh_pool_data(PL.pool), fh_pool_bytes(PL.pool)) == FSCLG_OK;
+    if (!PL.registered)
+      logmsg(MSG_WARN, "fscl_amd: the permutation pool could not be page-locked (%s): rows are copied to the "
+                       "device staging\n", fsclg_last_error());
+  }
+  if (D.rank != 0) return;
+  if (!SP.pb_in_pool)
+    for (b = 0; b < SP.n_pb; b++) { fsclg_host_free(SP.pb[b].buf); free(SP.pb[b].nul); }
+  for (b = 0; b < nbuf; b++) {
+    char *base = fh_pool_data(PL.pool) + (size_t)b * (rows + nulb);
+    SP.pb[b].buf = base;
+    SP.pb[b].nul = (double *)(base + rows);
+    SP.pb[b].owner = PB_FREE;
+  }
+  SP.n_pb = nbuf;
+  SP.pb_in_pool = 1;
+  SP.pb_cap = n_snps; SP.pb_nchr = D.n_chr; SP.pb_rb = D.rb;
+}
+
+static void pool_drop(void) {
+  if (!PL.pool) return;
+  if (SP.pb_in_pool) { SP.n_pb = 0; SP.pb_in_pool = 0; SP.pb_cap = 0; }
+  if (PL.registered) fsclg_host_unregister(fh_pool_data(PL.pool));
+  fh_pool_close(PL.pool);
+  PL.pool = NULL;
+  PL.registered = 0;
 }
 
 /* no candidate running (cancelled ones included): the buffers are the caller's again */
@@ -1000,7 +1089,7 @@ static void tb_reserve(trial_batch_t *b, int n) {
   b->cap = n;
   b->pt = fh_realloc(b->pt, sizeof(int) * n, "batch");
   b->cells = fh_realloc(b->cells, sizeof(fsclg_cell_t) * n, "batch");
-  b->out = fh_realloc(b->out, sizeof(fsclg_point_t) * n, "batch");
+  b->out = fh_realloc(b->out, sizeof(fsclg_point_t) * (n + 1), "batch");  /* + the exchange's flag word */
 }
 
 static void tb_free(trial_batch_t *b) { free(b->pt); free(b->cells); free(b->out); memset(b, 0, sizeof *b); }
@@ -1046,15 +1135,15 @@ static void tb_submit(trial_batch_t *b, int slot, int eval_range, int bp_resl) {
   b->submitted = 1;
 }
 
-/* wait for a batch and file each result in its point's queue */
-static void tb_wait(trial_batch_t *b, pqueue_t *pq) {
+/* wait for a batch and file each result in its point's queue; `flags`: see exchange_points_flags */
+static void tb_wait_flags(trial_batch_t *b, pqueue_t *pq, unsigned *flags) {
   int k, l;
   double tw = fh_now();
   if (!b->submitted) return;
   for (l = 0; l < D.n_dev; l++) dev_check(fsclg_search_wait(D.ctx[l], b->batch, b->out + b->lo[l]), "search wait");
   b->submitted = 0;
   D.st.wait_s += fh_now() - tw;
-  exchange_points(b->out, b->n, b->lo[0], b->hi[D.n_dev - 1]);
+  exchange_points_flags(b->out, b->n, b->lo[0], b->hi[D.n_dev - 1], flags);
   if (g_pcost)
     for (k = 0; k < b->n; k++) g_pcost[b->pt[k]] = (double)b->out[k].cost;
   for (k = 0; k < b->n; k++) {
@@ -1070,6 +1159,8 @@ static void tb_wait(trial_batch_t *b, pqueue_t *pq) {
     if (j == q->n) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline lost a result");
   }
 }
+
+static void tb_wait(trial_batch_t *b, pqueue_t *pq) { tb_wait_flags(b, pq, NULL); }
 
 /* apply point i's queued results in trial order, up to trial `upto`; only trial `draw`
    may draw rand() (scan-chromosome.c:488-502) */
@@ -1153,9 +1244,13 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   double tr[8];
   unsigned long long draw_mark = 0;
   int posted = 0, from_spec, bi;
+  unsigned sig = 0;
+  double *pnul;
+  PL.on = perm_leader_wanted();
   spec_start();
   D.st.spec_threads = SP.n_th;
-  pb_reserve(s->n_snps, K);
+  if (PL.on) pool_setup(s->n_snps, K);
+  else pb_reserve(s->n_snps, K);
   SP.snps = s->snps; SP.n = s->n_snps; SP.nbp = permute_nbp; SP.width_mb = scan_width_mb;
   for (;;) {
     const int slot = (trial + 1) % K;
@@ -1172,15 +1267,36 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     tp = fh_now();
     tr[1] = tp;
     slot_release(slot);
-    /* this trial's permutation: the candidate for the previous trial's draw count, else built here */
-    bi = posted ? spec_take((int)(g_draws - draw_mark), g) : -1;
-    from_spec = bi >= 0;
-    if (bi < 0) {
-      bi = pb_get();
-      block_permute(SP.pb[bi].buf, D.rowp, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
+    if (PL.on && D.rank != 0) {
+      /* the leader's permutation of this trial: its rows, its null sums, and the rand() state
+         after it (the prune draws that follow are this rank's own, the same as the leader's) */
+      size_t ro, no;
+      unsigned long long nj;
+      if (fh_pool_take(PL.pool, &ro, &no, g, &nj) != 0) logmsg(MSG_FATAL, "fscl_amd: permutation pool: no leader");
+      D.st.negj += nj;
+      prow = fh_pool_data(PL.pool) + ro;
+      pnul = (double *)(fh_pool_data(PL.pool) + no);
+      from_spec = 1;  /* the null sums come with it */
+    } else {
+      const unsigned long long negj0 = D.st.negj;
+      /* this trial's permutation: the candidate for the previous trial's draw count, else built here */
+      bi = posted ? spec_take((int)(g_draws - draw_mark), g) : -1;
+      from_spec = bi >= 0;
+      if (bi < 0) {
+        bi = pb_get();
+        block_permute(SP.pb[bi].buf, D.rowp, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
+      }
+      SP.pb[bi].owner = slot;
+      prow = SP.pb[bi].buf;
+      pnul = SP.pb[bi].nul;
+      if (PL.on) {  /* the leader: complete and publish it */
+        if (!from_spec) chr_null_sums(prow, pnul);
+        from_spec = 1;
+        if (fh_pool_publish(PL.pool, (size_t)((char *)prow - fh_pool_data(PL.pool)),
+                            (size_t)((char *)pnul - fh_pool_data(PL.pool)), g, D.st.negj - negj0) != 0)
+          logmsg(MSG_FATAL, "fscl_amd: permutation pool: a rank stopped taking permutations");
+      }
     }
-    SP.pb[bi].owner = slot;
-    prow = SP.pb[bi].buf;
     D.st.host_perm_s += fh_now() - tp;
     trial++;
     for (i = k = 0; i < n_act; i++)
@@ -1190,10 +1306,14 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     if (n_act == 0 || trial > n_perm) break;
     tp = fh_now();
     tr[2] = tp;
-    if (!from_spec) chr_null_sums(prow, SP.pb[bi].nul);  /* a candidate carries its own */
+    if (!from_spec) chr_null_sums(prow, pnul);  /* a candidate carries its own */
     D.st.host_null_s += fh_now() - tp;
-    memcpy(nul[slot], SP.pb[bi].nul, sizeof(double) * (D.n_chr ? D.n_chr : 1));
+    memcpy(nul[slot], pnul, sizeof(double) * (D.n_chr ? D.n_chr : 1));
     tp = fh_now();
+    if (PL.on && !PL.registered) {  /* the pool is not page-locked here: through the slot's own staging */
+      memcpy(D.stage[slot], prow, (size_t)D.rb * (size_t)s->n_snps);
+      prow = D.stage[slot];
+    }
     slot_upload_buf(slot, prow, nul[slot]);
     D.st.host_upload_s += fh_now() - tp;
     tp = fh_now();
@@ -1224,7 +1344,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     tb_submit(&A, slot, eval_range, bp_resl);
     tb_submit(B, slot, eval_range, bp_resl);
     /* while the GPUs work: the next trial's permutation for this trial's likely draw counts */
-    posted = SP.n_th > 0;
+    posted = SP.n_th > 0 && !(PL.on && D.rank != 0);  /* with the leader's permutations only the leader speculates */
     if (posted) {
       int dl[SPEC_MAX];
       spec_post(g, dl, spec_candidates(s, pq, &A, SP.n_th, dl));
@@ -1234,7 +1354,11 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       int drain = 0, m = 0;
       for (k = 0; k < A.n; k++) m += s->scan_pts[A.pt[k]].permute_p + pq[A.pt[k]].n >= 20;
       tr[4] = fh_now();
-      tb_wait(&A, pq);
+      /* the blocking batch's exchange (made every trial, even for no cells) carries each rank's
+         SIGINT flag: every rank gets the OR, so all dump at the same trial (no extra collective) */
+      sig = g_sigint ? 1u : 0u;
+      tb_wait_flags(&A, pq, &sig);
+      if (D.world <= 1 || D.sim) sig = g_sigint ? 1u : 0u;
       tr[5] = fh_now();
       /* a point that may draw in this trial needs every earlier result applied first */
       for (k = 0; k < A.n && !drain; k++) {
@@ -1265,7 +1389,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       fprintf(tt, "%d %d %d %d %.0f %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n", trial, n_act, A.n, B->n,
               (tr[1] - tr[0]) * 1e6, (tr[2] - tr[1]) * 1e6, (tr[3] - tr[2]) * 1e6, (tr[4] - tr[3]) * 1e6,
               (tr[5] - tr[4]) * 1e6, (fh_now() - tr[5]) * 1e6, tr[6], tr[7]);
-    if (sigint_agreed()) {
+    if (sig) {
       /* the dump shows every trial up to this one: the bulk results still in flight first
          (no draws among them) */
       for (;;) {
@@ -1294,6 +1418,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     if (pq[i].n) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline: unapplied results");
   for (k = 0; k < K; k++) slot_release(k);  /* every upload has read its buffer */
   spec_quiesce();
+  PL.on = 0;
   if (tt) fclose(tt);
   tb_free(&A);
   for (k = 0; k < K; k++) { tb_free(&Bt[k]); free(nul[k]); }
@@ -1928,6 +2053,7 @@ void fscl_amd_reset_stats(void) {
 }
 
 void fscl_amd_shutdown(void) {
+  pool_drop();
   spec_stop();
   dev_close_all();
   if (DI.ctx) fsclg_close(DI.ctx);

@@ -42,27 +42,73 @@ def _neutral_counts(rng: np.random.Generator, n: int, count: int) -> np.ndarray:
     return rng.choice(np.arange(1, n), size=count, p=p)
 
 
+def ascertained(rng: np.random.Generator, k: np.ndarray, n: int, asc_depth: int, asc_min_freq: int) -> np.ndarray:
+    """Which sites an ascertainment panel of ``asc_depth`` of the n haplotypes would discover.
+
+    The reference simulates ascertainment exactly this way (ascbias-segments.c:88-101): the
+    first asc_depth haplotypes form the panel, d = derived copies among them, and with
+    ``double_hit`` a site is kept iff 1 < d < asc_depth - 1, i.e. both alleles seen at least
+    twice.  fscl's correction models the same event with K = --asc-minimum-freq
+    (asc-bias.c:12-25: not ascertained iff d < K or asc_depth - d < K).  A random panel of
+    haplotypes makes d hypergeometric(k derived, n - k ancestral, asc_depth draws)."""
+    d = rng.hypergeometric(k, n - k, asc_depth)
+    return (d >= asc_min_freq) & (asc_depth - d >= asc_min_freq)
+
+
+def _chromosome_ascertained(rng, chr_len, count, n, sweeps_per_chr, sweep_scale, asc_depth, asc_min_freq):
+    """One chromosome of ``count`` ascertained sites: a larger pool of sites (neutral spectrum,
+    planted sweeps) is drawn, every site goes through the panel filter (ascertained()), and
+    ``count`` of the kept sites are taken.  Planted-sweep sites go through the same filter; they
+    are set to extreme but ascertainable counts (2..6 copies of one allele) instead of the
+    unascertainable singletons of the unascertained configurations."""
+    pool = 3 * count + 64
+    while True:
+        if pool > chr_len:
+            raise ValueError("chromosome too short for the ascertained site count")
+        pos = _positions(rng, chr_len, pool)
+        k = _neutral_counts(rng, n, pool)
+        for _ in range(sweeps_per_chr):
+            centre = rng.integers(1, chr_len + 1)
+            d = np.abs(pos - centre).astype(np.float64)
+            hit = rng.random(pool) < np.exp(-d / sweep_scale)
+            hi = rng.random(pool) < 0.15
+            x = rng.integers(2, 7, size=pool)
+            k = np.where(hit, np.where(hi, n - x, x), k)
+        keep = np.nonzero(ascertained(rng, k, n, asc_depth, asc_min_freq))[0]
+        if keep.size >= count:
+            sel = np.sort(rng.choice(keep, size=count, replace=False))
+            return pos[sel], k[sel]
+        pool *= 2
+
+
 def generate(n_chr: int, chr_len: int, snps_per_chr: int, n: int, folded: float = 0.0,
              seed: int = 1, sweeps_per_chr: int = 0, sweep_scale: float = 20_000.0,
              chr_names: list[str] | None = None, missing: float = 0.0, max_missing: int = 4,
-             duplicates: float = 0.0, **_unused):
+             duplicates: float = 0.0, asc_depth: int = 0, asc_min_freq: int = 1, **_unused):
     """Return a list of per-chromosome (name, pos, k, n_arr, folded_arr) arrays.
 
     ``missing``: fraction of sites whose sample size is n - U{1..max_missing}
     (several sample depths, as with missing genotypes); ``duplicates``: fraction
-    of sites moved onto the previous site's position (ties in position)."""
+    of sites moved onto the previous site's position (ties in position);
+    ``asc_depth`` > 0: only sites an ascertainment panel of that many haplotypes
+    discovers with both alleles seen ``asc_min_freq`` times (ascertained(): the data
+    that fscl's -d / --asc-minimum-freq correction models), ``snps_per_chr`` of them."""
     rng = np.random.default_rng(seed)
     out = []
     for c in range(n_chr):
         name = chr_names[c] if chr_names else f"chr{c + 1}"
-        pos = _positions(rng, chr_len, snps_per_chr)
-        k = _neutral_counts(rng, n, snps_per_chr)
-        for _ in range(sweeps_per_chr):
-            centre = rng.integers(1, chr_len + 1)
-            d = np.abs(pos - centre).astype(np.float64)
-            hit = rng.random(snps_per_chr) < np.exp(-d / sweep_scale)
-            hi = rng.random(snps_per_chr) < 0.15
-            k = np.where(hit, np.where(hi, n - 1, 1), k)
+        if asc_depth > 0:
+            pos, k = _chromosome_ascertained(rng, chr_len, snps_per_chr, n, sweeps_per_chr, sweep_scale,
+                                             asc_depth, asc_min_freq)
+        else:
+            pos = _positions(rng, chr_len, snps_per_chr)
+            k = _neutral_counts(rng, n, snps_per_chr)
+            for _ in range(sweeps_per_chr):
+                centre = rng.integers(1, chr_len + 1)
+                d = np.abs(pos - centre).astype(np.float64)
+                hit = rng.random(snps_per_chr) < np.exp(-d / sweep_scale)
+                hi = rng.random(snps_per_chr) < 0.15
+                k = np.where(hit, np.where(hi, n - 1, 1), k)
         fold = (rng.random(snps_per_chr) < folded).astype(np.int64)
         nn = np.full(snps_per_chr, n, dtype=np.int64)
         if missing > 0:

@@ -138,6 +138,13 @@ int fsclg_search_wait(fsclg_ctx *c, int batch, fsclg_point_t *out);
    context it was handed to (the slot's last upload has read it). */
 void *fsclg_host_alloc(size_t bytes);
 void fsclg_host_free(void *p);
+/* The same for memory the caller mapped itself (a POSIX shared-memory segment that several
+   processes map: one node leader builds each trial's rows once, every rank's devices read
+   them): page-locks [p, p + bytes) for every device (portable, mapped).  Returns FSCLG_OK only
+   if the devices address the memory by the same pointer (the pointer can go to
+   fsclg_slot_set_rows_packed as it is); fsclg_host_unregister undoes it. */
+int fsclg_host_register(void *p, size_t bytes);
+int fsclg_host_unregister(void *p);
 int fsclg_slot_wait(fsclg_ctx *c, int slot);
 int fsclg_slot_set_rows_host(fsclg_ctx *c, int slot, const uint32_t *row, const double *chr_null);
 /* the same with rows of row_bytes = 1, 2 or 4 bytes each (1: n_rows <= 256, 2: n_rows <= 65536):

@@ -55,12 +55,19 @@ CASES = {
     "C5_full_p25": dict(gen=dict(n_chr=22, chr_len=227_272_727, snps_per_chr=227_273, n=400, folded=0.0, seed=55,
                                  sweeps_per_chr=2), opts=["--n-permute=25"]),
     # bench.py --config C2 / C3, exactly (seed 1, 100 permutations; C3 with its ascertainment
-    # options): their bench lines check every timed job against these digests too
+    # options, on ascertained sites -- synth.ascertained(), the reference's double-hit panel rule
+    # ascbias-segments.c:88-101): their bench lines check every timed job against these digests too
     "C2_bench_p100": dict(gen=dict(n_chr=1, chr_len=200_000_000, snps_per_chr=100_000, n=100, folded=0.0, seed=1,
                                    sweeps_per_chr=2), opts=["--n-permute=100"]),
     "C3_bench_p100": dict(gen=dict(n_chr=1, chr_len=200_000_000, snps_per_chr=100_000, n=100, folded=0.3, seed=1,
-                                   sweeps_per_chr=2),
+                                   sweeps_per_chr=2, asc_depth=20, asc_min_freq=2),
                           opts=["--n-permute=100", "--asc-depth=20", "--asc-minimum-freq=2"]),
+    # configs[4]'s permutation regime at its real depth: one whole C5 chromosome (chromosome 1 of
+    # the seed-55 genome, i.e. bench.py --config C5 --chromosomes 1 --seed 55) with 10 000
+    # permutations -- the early-prune tail: survivors running thousands of trials, per-trial
+    # windowed null sums on few cells (scan-chromosome.c:412-546, prune :488-498, windows :92-94)
+    "C5_chr_p10000": dict(gen=dict(n_chr=1, chr_len=227_272_727, snps_per_chr=227_273, n=400, folded=0.0, seed=55,
+                                   sweeps_per_chr=2), opts=["--n-permute=10000"]),
 }
 
 
@@ -95,7 +102,6 @@ def main(argv: list[str]) -> int:
             names.append(a)
     names = names or list(CASES)
     fx_path = HERE / "fullsize.json"
-    fx = json.loads(fx_path.read_text()) if fx_path.exists() else {}
     for name in names:
         c = CASES[name]
         with tempfile.TemporaryDirectory() as d:
@@ -107,6 +113,8 @@ def main(argv: list[str]) -> int:
                             *c["opts"], f"--dump-points={d / 'o.dump'}"], check=True, capture_output=True)
             dt = time.time() - t0
             rows = read_dump(d / "o.dump")
+            # re-read at write time: cases run concurrently (hours apart) must not drop each other's entries
+            fx = json.loads(fx_path.read_text()) if fx_path.exists() else {}
             fx[name] = dict(gen=c["gen"], options=c["opts"], input_sha256=sha256_file(snp),
                             dump_sha256=canonical_dump(rows), out_sha256=sha256_file(d / "o.txt"),
                             n_points=len(rows), sum_permute_n=sum(r[10] for r in rows),

@@ -269,26 +269,34 @@ def test_search_maxalpha_dropin(built):
     assert t_pts < 1e-3 * len(rows)
 
 
-@pytest.mark.parametrize("exchange", ["callback", "shm"])
+@pytest.mark.parametrize("exchange", ["callback", "shm", "shm_replicated"])
 def test_two_ranks_on_one_gpu_match_one_rank(built, tmp, exchange):
     """Parity mode with 2 processes (both on GPU 0): the exchange through a Python gloo
-    callback, or the library's own shared-memory all-gather."""
+    callback, or the library's own shared-memory all-gather.  With the shared-memory exchange
+    rank 0 builds every trial's permutation once into the node's shared pool and rank 1's device
+    reads it (FSCL_AMD_PERM_LEADER=0, "shm_replicated": each rank builds its own)."""
     c = manifest()["cases"]["g1_p25"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 1000), WORLD_SIZE="2",
                FSCL_AMD_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0", FSCL_AMD_RANK_TIMEOUT="120")
-    if exchange == "shm":
+    if exchange.startswith("shm"):
         env["FSCL_MR_SHM"] = f"/fscl_amd_mr_{os.getpid()}"
+    if exchange == "shm_replicated":
+        env["FSCL_AMD_PERM_LEADER"] = "0"
     procs = []
     for r in range(2):
         e = dict(env, RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, str(ROOT / "tests" / "mr_worker.py"), str(GOLD / c["input"]),
                                        str(tmp / f"o{r}.txt"), *c["options"]], env=e, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
+    errs = []
     for p in procs:
         out, err = p.communicate(timeout=600)
         assert p.returncode == 0, err
+        errs.append(err)
     assert (tmp / "o0.txt").read_text() == (GOLD / "g1_p25.out").read_text()
     assert not (tmp / "o1.txt").exists()  # one writer
+    if exchange == "shm":  # the leader's permutations: rank 1 builds none (no speculation threads)
+        assert "spec_threads 0" in errs[1], errs[1][-400:]
 
 
 def test_pipelined_trials_match_lockstep_and_oracle(built, tmp, monkeypatch):
@@ -329,8 +337,9 @@ def test_c2_scale_scan_and_short_permutation(built, tmp):
 
 
 @pytest.mark.parametrize("name,gen,opts", [
-    # BASELINE config 3 at full size: ascertainment K=2 of M=20, 30 % folded sites
-    ("C3", dict(n_chr=1, chr_len=200_000_000, snps_per_chr=100_000, n=100, folded=0.3, seed=3, sweeps_per_chr=2),
+    # BASELINE config 3 at full size: ascertainment K=2 of M=20 (on ascertained sites), 30 % folded
+    ("C3", dict(n_chr=1, chr_len=200_000_000, snps_per_chr=100_000, n=100, folded=0.3, seed=3, sweeps_per_chr=2,
+                asc_depth=20, asc_min_freq=2),
      ["--asc-depth=20", "--asc-minimum-freq=2", "--n-permute=2"]),
     # one chromosome of BASELINE config 5 (227k SNPs, n=400): every point's window is a
     # proper 2*81920+1-SNP window of the chromosome (per-window null sums on the device)
@@ -688,6 +697,22 @@ def test_split_timeout_reruns_unsplit(built, tmp, monkeypatch):
     fscl_amd.reset_stats()
     fscl_amd.run(GOLD / c["input"], tmp / "g.txt", **_kw(c["options"]))
     assert fscl_amd.get_stats()["n_split_retry"] == 3
+    assert (tmp / "g.txt").read_text() == (GOLD / "g1_p25.out").read_text()
+
+
+def test_split_member_late_past_the_wait_is_flagged(built, tmp, monkeypatch):
+    """A real timeout, not a forced one: member 0 of cell 0 of every split launch
+    sleeps 30 ms before its first arrival (FSCLG_TEST_SPLIT_DELAY_US) while the others wait only
+    3 ms (FSCLG_SPLIT_WAIT_US).  The others time out, go on with partial sums and publish the
+    timeout in the cell's arrival word; member 0, whose own wait is then satisfied at once by
+    their arrivals, must still flag its point, so the launch is re-run unsplit: the output is
+    the golden one and the re-runs are counted."""
+    c = manifest()["cases"]["g1_p25"]
+    monkeypatch.setenv("FSCLG_TEST_SPLIT_DELAY_US", "30000")
+    monkeypatch.setenv("FSCLG_SPLIT_WAIT_US", "3000")
+    fscl_amd.reset_stats()
+    fscl_amd.run(GOLD / c["input"], tmp / "g.txt", **_kw(c["options"]))
+    assert fscl_amd.get_stats()["n_split_retry"] >= 1
     assert (tmp / "g.txt").read_text() == (GOLD / "g1_p25.out").read_text()
 
 

@@ -168,3 +168,97 @@ def test_shared_memory_exchange_flags_and_divergence(built, tmp_path):
         assert p.returncode == 0, err
         assert "ok" in out.split(), out
         assert "rank exchange mismatch" in err
+
+
+POOL_WORKER = r"""
+import ctypes as C, os, sys, time
+import numpy as np
+sys.path.insert(0, os.environ["REPO"])
+import fscl_amd
+L = fscl_amd.get_lib()
+L.fh_shm_open.restype = C.c_void_p
+L.fh_shm_open.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_size_t]
+L.fh_pool_open.restype = C.c_void_p
+L.fh_pool_open.argtypes = [C.c_void_p, C.c_size_t]
+L.fh_pool_data.restype = C.c_void_p
+L.fh_pool_data.argtypes = [C.c_void_p]
+L.fh_pool_bytes.restype = C.c_size_t
+L.fh_pool_bytes.argtypes = [C.c_void_p]
+Rand = C.c_int32 * 33  # fh_rand_t: r[31], f, b
+L.fh_srand.argtypes = [C.c_void_p, C.c_uint]
+L.fh_pool_publish.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_ulonglong]
+L.fh_pool_take.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.c_void_p,
+                           C.POINTER(C.c_ulonglong)]
+L.fh_pool_release.argtypes = [C.c_void_p]
+L.fh_pool_wait_released.argtypes = [C.c_void_p]
+L.fh_pool_close.argtypes = [C.c_void_p]
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+m = L.fh_shm_open(rank, world, os.environ["SHM_NAME"].encode(), 1 << 16)
+assert m, "attach"
+NB, BUF, K, T = 6, 4096, 4, 300
+p = L.fh_pool_open(m, NB * BUF if rank == 0 else 0)
+assert p and L.fh_pool_bytes(p) >= NB * BUF
+base = L.fh_pool_data(p)
+owner = [-1] * NB          # leader: the slot whose trial reads each buffer
+slot_buf = [None] * K
+rng = np.random.default_rng(rank)
+for t in range(T):
+    slot = t % K
+    if t >= K:             # the slot's previous trial: this rank is done reading it
+        L.fh_pool_release(p)
+        if rank == 0:
+            assert L.fh_pool_wait_released(p) == 0
+            for b in range(NB):
+                if owner[b] == slot:
+                    owner[b] = -1
+    if rank == 0:          # build trial t's "permutation" into a free buffer and publish it
+        b = owner.index(-1)
+        owner[b] = slot
+        arr = np.frombuffer((C.c_char * BUF).from_address(base + b * BUF), dtype=np.uint8)
+        arr[:] = t % 251
+        g = Rand()
+        L.fh_srand(g, t + 1)
+        assert L.fh_pool_publish(p, b * BUF, b * BUF + 8, g, t) == 0
+        slot_buf[slot] = b * BUF
+    else:
+        ro, no, nj = C.c_size_t(), C.c_size_t(), C.c_ulonglong()
+        g = Rand()
+        assert L.fh_pool_take(p, C.byref(ro), C.byref(no), g, C.byref(nj)) == 0
+        want = Rand()
+        L.fh_srand(want, t + 1)
+        assert bytes(g) == bytes(want) and nj.value == t and no.value == ro.value + 8
+        slot_buf[slot] = ro.value
+    if rng.random() < 0.2:
+        time.sleep(0.001)  # ranks out of step
+    # every rank "reads" its slots still in flight: none was overwritten
+    for back in range(min(K, t + 1)):
+        tr = t - back
+        arr = np.frombuffer((C.c_char * BUF).from_address(base + slot_buf[tr % K]), dtype=np.uint8)
+        assert (arr[16:] == tr % 251).all(), (rank, t, tr)
+for k in range(K):
+    L.fh_pool_release(p)
+if rank == 0:
+    assert L.fh_pool_wait_released(p) == 0
+L.fh_pool_close(p)
+print("ok", rank)
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_permutation_pool_protocol(built, tmp_path, world):
+    """ranks.c's node-leader pool: rank 0 writes 300 trials' buffers into a
+    shared segment and publishes each with a rand() state; the other ranks take them in order
+    (state and count intact) and release their row slots.  A buffer is reused only after every
+    rank released the slot that read it: every rank checks, every trial, that the K trials it
+    still has in flight keep their contents while the ranks drift out of step."""
+    script = tmp_path / "p.py"
+    script.write_text(POOL_WORKER)
+    env = dict(os.environ, WORLD_SIZE=str(world), REPO=str(ROOT), SHM_NAME=f"/fscl_amd_testp_{os.getpid()}_{world}",
+               FSCL_AMD_RANK_TIMEOUT="60")
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(world)]
+    for p in procs:
+        out, err = p.communicate(timeout=300)
+        assert p.returncode == 0, err
+        assert "ok" in out.split(), out
+    assert not list(Path("/dev/shm").glob(f"fscl_amd_testp_{os.getpid()}_{world}*"))
