@@ -2988,6 +2988,12 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
       }
       std::vector<int> lists[8];
       for (int u : B.order) lists[cls[u]].push_back(u);
+      // FSCLG_XCD_ORDER=1 (A/B): chromosome-major within a class -- an XCD then works on one of
+      // its chromosomes at a time (its L2 holds one site array instead of its run's 3 at C5)
+      static const int chr_major = getenv("FSCLG_XCD_ORDER") ? atoi(getenv("FSCLG_XCD_ORDER")) : 0;
+      if (chr_major)
+        for (auto& l : lists)
+          std::stable_sort(l.begin(), l.end(), [&](int x, int y) { return B.ucells[x].chr < B.ucells[y].chr; });
       size_t L = 0;
       for (auto& l : lists) L = std::max(L, l.size());
       B.order.assign(8 * L, -1);

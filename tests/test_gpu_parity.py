@@ -186,21 +186,33 @@ def test_tiny_chromosomes_match_oracle(built, tmp):
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
 
 
-def test_ms_input_matches_oracle_on_converted_file(built, tmp):
+@pytest.mark.parametrize("name,blocks,hap,seg,length,grid", [
+    ("blocks", 4, 20, 600, 2_000_000, 50_000),
+    # BASELINE configs[0] as specified: one ms-simulated 10k-site block, n=50, a 20 Mb segment,
+    # the default 100 kb grid (200 grid points), no permutations
+    ("C1", 1, 50, 10_000, 20_000_000, 100_000),
+])
+def test_ms_input_matches_oracle_on_converted_file(built, tmp, name, blocks, hap, seg, length, grid):
+    """The ms path (ms-input.c:93-151, semantics defined in DESIGN.md §6: the reference's is
+    non-functional) against the oracle on the same sites written as an SNP file."""
     ms = tmp / "x.ms"
-    synth.write_ms_file(str(ms), n_blocks=4, n_hap=20, n_seg=600, seed=41)
-    scan = fscl_amd.load_ms_input(ms, 2_000_000)
+    synth.write_ms_file(str(ms), n_blocks=blocks, n_hap=hap, n_seg=seg, seed=41)
+    scan = fscl_amd.load_ms_input(ms, length)
     s = scan.contents
     depth = s.sample_depths[0]
+    assert s.n_chromosomes == blocks and s.n_snps > 0.95 * blocks * seg
     with open(tmp / "x.snp", "w") as f:  # the same sites as an SNP file
         for i in range(s.n_snps):
             p = s.snps[i]
             f.write(f"{s.chr_limits[p.chr].name.decode()} {p.pos} {p.obs_freq} {depth} {p.folded}\n")
-    r = subprocess.run([str(CLI), "-m", str(ms), "--ms-segment-length=2000000", "-o", str(tmp / "g.txt"),
-                        "-G", "50000"], capture_output=True, text=True, timeout=600)
+    r = subprocess.run([str(CLI), "-m", str(ms), f"--ms-segment-length={length}", "-o", str(tmp / "g.txt"),
+                        "-G", str(grid)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr
-    run_oracle(tmp / "x.snp", tmp / "o.txt", ["--coarse-grid-spacing=50000"])
-    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+    run_oracle(tmp / "x.snp", tmp / "o.txt", [f"--coarse-grid-spacing={grid}"])
+    out = (tmp / "g.txt").read_text()
+    assert out == (tmp / "o.txt").read_text()
+    if name == "C1":
+        assert len(out.splitlines()) == 200
 
 
 def test_ms_block_loop_matches_whole_file(built, tmp):
@@ -438,6 +450,10 @@ def test_full_genomes_match_oracle_fixture(built, tmp, name):
     assert sha256_file(tmp / "g.txt") == fx["out_sha256"]
     if name.startswith("C5"):
         assert fscl_amd.get_stats()["window_ms"] > 0
+    if name == "C3_bench_p100":  # a real workload: ascertained sites give CLRs, points outlive trial 20
+        clr = np.array([r[2] for r in rows])
+        assert (clr != 0.0).mean() >= 0.95, (clr != 0.0).mean()
+        assert max(r[10] for r in rows) > 21
 
 
 @pytest.fixture

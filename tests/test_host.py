@@ -352,3 +352,28 @@ def test_chunked_window_sums_are_the_sequential_sums():
         for i in range(a, a + W):
             seq = seq + v[i]
         assert _chunked_window_sum(v, W, a, emin, ne).hex() == seq.hex(), a
+
+
+def test_c3_input_is_ascertained_and_its_fixture_is_not_degenerate():
+    """BASELINE configs[2] (K=2 of M=20 ascertainment correction) runs on ascertained sites
+    (synth.ascertained: the reference's double-hit panel rule, ascbias-segments.c:88-101):
+    100 000 sites, none with fewer than 2 copies of either allele -- on unascertained sites
+    every C3 CLR was 0.0.  The oracle's run of bench.py's C3 job
+    (tests/golden/fullsize.json[C3_bench_p100]) has non-zero CLRs and points that outlive
+    trial 20 (the prune tail), in its sampled rows and its permutation count."""
+    import json
+    cfg = dict(synth.CONFIGS["C3"])
+    (name, pos, k, nn, fold), = synth.generate(seed=1, sweeps_per_chr=2, **cfg)
+    assert len(pos) == cfg["snps_per_chr"] and (np.diff(pos) > 0).all()
+    assert np.minimum(k, nn - k).min() >= cfg["asc_min_freq"]
+    # the filter itself: a site is kept iff both alleles appear >= K times in the M-panel
+    rng = np.random.default_rng(0)
+    kk = np.arange(1, 100)
+    keep = np.array([synth.ascertained(rng, np.full(4000, x), 100, 20, 2).mean() for x in kk])
+    assert keep[0] == 0.0 and keep[-1] == 0.0 and keep[49] > 0.99
+    fx = json.loads((GOLD / "fullsize.json").read_text())["C3_bench_p100"]
+    assert fx["gen"].get("asc_depth") == 20 and fx["gen"].get("asc_min_freq") == 2
+    rows = [r.split("\t") for r in fx["sample"]]
+    assert all(float.fromhex(r[2]) != 0.0 for r in rows)
+    assert fx["sum_permute_n"] > 21 * fx["n_points"]
+    assert max(int(r[10]) for r in rows) > 21
