@@ -62,7 +62,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C4")
     ap.add_argument("--n-permute", type=int, default=None)
-    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=None,
+                    help="synthetic genome seed (default 55 for C5 -- the seed of its oracle fixtures -- else 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU baseline threads (default: every CPU this process may run on)")
@@ -258,6 +259,8 @@ def main() -> int:
         fscl_amd.set_device(device)
     n_gpus = world * n_local
 
+    if args.seed is None:
+        args.seed = 55 if args.config == "C5" else 1
     cfg = dict(synth.CONFIGS[args.config])
     if args.chromosomes:
         cfg["n_chr"] = args.chromosomes

@@ -192,13 +192,19 @@ int main(int argc, char **argv) {
       /* one process per GPU (e.g. under torch.distributed.run): GPU $LOCAL_RANK (or
          $FSCL_AMD_DEVICE), results exchanged through a shared-memory segment named by
          $FSCL_AMD_SHM_NAME, else the launcher's run id or port; rank 0 writes the output */
-      const char *id = getenv("FSCL_AMD_SHM_NAME"), *run = getenv("TORCHELASTIC_RUN_ID"), *port = getenv("MASTER_PORT");
+      const char *id = getenv("FSCL_AMD_SHM_NAME"), *run = getenv("TORCHELASTIC_RUN_ID"), *port = getenv("MASTER_PORT"),
+                 *addr = getenv("MASTER_ADDR"), *sj = getenv("SLURM_JOB_ID"), *ss = getenv("SLURM_STEP_ID");
       char name[200];
       if (id) snprintf(name, sizeof name, "/fscl_amd_%s", id);
-      else /* the launcher's run id (plain torchrun sets "none"), its port, and the parent's pid: the
-              ranks of one launch share their parent (the launcher), two jobs on a node do not */
-        snprintf(name, sizeof name, "/fscl_amd_%s_%s_%ld", run && strcmp(run, "none") ? run : "job", port ? port : "0",
-                 (long)getppid());
+      else if (port || (run && strcmp(run, "none")) || sj)
+        /* values a launcher gives every rank of one job alike, and two concurrent jobs on a node
+           not: the rendezvous port (torch.distributed.run, mpirun wrappers), the launcher's run id
+           (plain torchrun sets "none"), the Slurm job and step -- not the parent's pid, which
+           differs between ranks started through a per-rank wrapper (a shell script, srun) */
+        snprintf(name, sizeof name, "/fscl_amd_%s_%s_%s_%s_%s", run && strcmp(run, "none") ? run : "job",
+                 addr ? addr : "-", port ? port : "0", sj ? sj : "-", ss ? ss : "-");
+      else /* no launcher variables: the ranks of one launch are assumed to share their parent */
+        snprintf(name, sizeof name, "/fscl_amd_job_%ld", (long)getppid());
       if (n_gpus > 1) logmsg(MSG_WARN, "Warning: --n-gpus is ignored with one process per GPU (WORLD_SIZE=%s).\n", ws);
       if (fscl_amd_set_ranks_shm(atoi(rk), atoi(ws), name) != 0)
         logmsg(MSG_FATAL, "fscl: rank %s of %s could not meet the other ranks (%s)", rk, ws, name);

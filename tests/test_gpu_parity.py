@@ -503,6 +503,25 @@ def test_cli_one_process_per_gpu(built, tmp):
     assert (tmp / "o.txt").read_text() == (GOLD / "g1_p25.out").read_text()
 
 
+def test_cli_ranks_meet_without_a_segment_name(built, tmp):
+    """No FSCL_AMD_SHM_NAME, each rank started through its own wrapper shell (different parent
+    processes, as with a per-rank script under torchrun --no-python or srun): the default segment
+    name comes from the launcher's variables (MASTER_ADDR / MASTER_PORT here), so the ranks
+    still meet, and rank 0 writes the golden output."""
+    import shlex
+    c = manifest()["cases"]["g1_p25"]
+    env = {k: v for k, v in os.environ.items() if k not in ("FSCL_AMD_SHM_NAME", "TORCHELASTIC_RUN_ID")}
+    env.update(WORLD_SIZE="2", FSCL_AMD_DEVICE="0", FSCL_AMD_RANK_TIMEOUT="120", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(31000 + os.getpid() % 2000))
+    cmd = " ".join(shlex.quote(str(a)) for a in [CLI, "-f", GOLD / c["input"], "-o", tmp / "o.txt", *c["options"]])
+    procs = [subprocess.Popen(["bash", "-c", f"{cmd}; exit $?"], env=dict(env, RANK=str(r), LOCAL_RANK="0"),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    for p in procs:
+        out, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err
+    assert (tmp / "o.txt").read_text() == (GOLD / "g1_p25.out").read_text()
+
+
 def test_cli_n_gpus(built, tmp):
     """fscl --n-gpus=1 and the CLI's default (every visible GPU) reproduce the golden output."""
     c = manifest()["cases"]["g1_p25"]
