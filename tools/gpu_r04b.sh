@@ -6,5 +6,5 @@ timeout -k 10 240 python bench.py --config C5 --chromosomes 1 --seed 55 --n-perm
 python3 -c "import json;d=json.load(open('gpurun_out/r04b/c5chr.json'));print('c5chr', d['ms_per_step'], d['value'])"
 timeout -k 10 120 python tools/shm_latency.py 8 3000 344 > gpurun_out/r04b/shm_latency8.json || exit 1
 cat gpurun_out/r04b/shm_latency8.json
-bash tools/rehearse.sh C4 r04b "8" "1 8" || exit 1
+bash tools/rehearse_ranks.sh C4 r04b 8 || exit 1
 bash tools/ab_xcd.sh r04b 2 || exit 1

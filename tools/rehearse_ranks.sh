@@ -1,0 +1,50 @@
+# Rehearsal of the driver's real 8-rank SCALE shape on one GPU (rehearsal build, run on the GPU box):
+#   bash tools/rehearse_ranks.sh <config> <tag> [W]
+# Records the job's batches once, then replays rank 0 of W three ways, each with the CPUs the
+# other W-1 ranks would take on this box's cgroup kept busy by spinning processes (a rank's main
+# thread spins in the exchanges), since the replay itself runs rank 0 alone:
+#   single  one process driving W GPUs (bench.py --gpus W without a launcher): every spare CPU
+#           speculates for the one host process, no other ranks;
+#   replicated  one process per GPU, each rank building its own permutations
+#           (FSCL_AMD_PERM_LEADER=0): rank 0 gets usable/W - 1 speculation threads, and the other
+#           ranks' main and speculation threads take the rest;
+#   leader  one process per GPU with the node leader's permutation pool (the default): rank 0
+#           speculates on usable - W threads, the other ranks' main threads take W - 1 CPUs.
+# The exchange latency the replay does not pay is measured separately (tools/shm_latency.py).
+set -o pipefail
+CFG=$1; TAG=$2; W=${3:-8}
+R=${GRAFT_REPO_ROOT:-$PWD}
+export FSCL_AMD_LIBDIR=$R/fscl_amd/_build_rehearsal
+OUT=$R/gpurun_out/ranks_$TAG
+mkdir -p $OUT
+REC=/tmp/fscl_sim_ranks_$TAG.bin
+U=$(python3 -c "import sys; sys.path.insert(0, '$R'); import bench; print(bench.cpu_info()['usable_cpus'])")
+echo "usable CPUs: $U, W=$W"
+timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > /dev/null 2>&1  # warm caches
+FSCL_AMD_SIM=record:$REC timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w1_record.json 2> $OUT/w1_record.err || exit 1
+burn() {  # $1 spinning processes, each time-limited; their pids in BURN_PIDS
+  BURN_PIDS=""
+  for i in $(seq $1); do
+    timeout -k 5 600 python3 -c "while True: pass" &
+    BURN_PIDS="$BURN_PIDS $!"
+  done
+}
+unburn() { for p in $BURN_PIDS; do kill $p 2>/dev/null; done; wait $BURN_PIDS 2>/dev/null; BURN_PIDS=""; }
+run() {  # <name> <spec threads> <burners>
+  burn $3
+  FSCL_AMD_SPEC=$2 FSCL_AMD_SIM=replay:$REC:$W:0 timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w${W}_$1_$4.json 2> $OUT/w${W}_$1_$4.err
+  local rc=$?
+  unburn
+  [ $rc -eq 0 ] || exit 1
+  echo "$1 (spec $2, $3 busy CPUs beside) round $4: $(python3 -c "import json;d=json.load(open('$OUT/w${W}_$1_$4.json'));s=d['stats'];print(round(d['ms_per_step']), 'ms/job; blocked on batches', round(s['wait_s'],3), 's; speculation', s['spec_hits'], '/', s['trials'], 'hits, wait', round(s['spec_wait_s'],3), 's')")"
+}
+SPEC_SINGLE=$((U - 1)); [ $SPEC_SINGLE -gt 32 ] && SPEC_SINGLE=32
+SPEC_REPL=$((U / W - 1)); [ $SPEC_REPL -lt 0 ] && SPEC_REPL=0
+SPEC_LEAD=$((U - W)); [ $SPEC_LEAD -lt 0 ] && SPEC_LEAD=0; [ $SPEC_LEAD -gt 32 ] && SPEC_LEAD=32
+BUSY_REPL=$(( (W - 1) * (SPEC_REPL + 1) ))
+for r in 1 2; do
+  run single $SPEC_SINGLE 0 $r
+  run replicated $SPEC_REPL $BUSY_REPL $r
+  run leader $SPEC_LEAD $((W - 1)) $r
+done
+rm -f $REC
