@@ -30,9 +30,9 @@ burn() {  # $1 spinning processes, each time-limited; their pids in BURN_PIDS
   done
 }
 unburn() { for p in $BURN_PIDS; do kill $p 2>/dev/null; done; wait $BURN_PIDS 2>/dev/null; BURN_PIDS=""; }
-run() {  # <name> <spec threads> <burners>
+run() {  # <name> <spec threads> <burners> <round> [env ...]
   burn $3
-  FSCL_AMD_SPEC=$2 FSCL_AMD_SIM=replay:$REC:$W:0 timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w${W}_$1_$4.json 2> $OUT/w${W}_$1_$4.err
+  env ${@:5} FSCL_AMD_SPEC=$2 FSCL_AMD_SIM=replay:$REC:$W:0 timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w${W}_$1_$4.json 2> $OUT/w${W}_$1_$4.err
   local rc=$?
   unburn
   [ $rc -eq 0 ] || exit 1
@@ -46,5 +46,7 @@ for r in 1 2; do
   run single $SPEC_SINGLE 0 $r
   run replicated $SPEC_REPL $BUSY_REPL $r
   run leader $SPEC_LEAD $((W - 1)) $r
+  # the split cells' speculative refine walks off
+  run leader_norefine $SPEC_LEAD $((W - 1)) $r FSCLG_SPEC_REFINE=0
 done
 rm -f $REC
