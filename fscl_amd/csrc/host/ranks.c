@@ -253,21 +253,30 @@ struct fh_pool {
 };
 
 /* collective (every rank of m, in the same order of calls): rank 0 creates a segment of
-   data_bytes (the others' argument is ignored: they map what rank 0 made) */
+   data_bytes (the others' argument is ignored: they map what rank 0 made).  Returns NULL on
+   every rank when rank 0 cannot reserve the memory (a small /dev/shm: the pages are allocated
+   up front, so a short tmpfs fails here instead of faulting later) */
 fh_pool_t *fh_pool_open(fh_shm_t *m, size_t data_bytes) {
-  char name[256];
+  char name[256], dummy = 0;
   fh_pool_t *p = fh_calloc(1, sizeof *p, "pool");
-  int fd = -1;
+  int fd = -1, err = 0;
+  unsigned fail = 0;
   p->m = m;
   snprintf(name, sizeof name, "%s_pool%u", m->name, m->n_pools++);
   if (m->rank == 0) {
     p->data_bytes = (data_bytes + 4095) & ~(size_t)4095;
     p->map_bytes = POOL_HDR + p->data_bytes;
     fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
-    if (fd < 0 || ftruncate(fd, (off_t)p->map_bytes) != 0)
-      logmsg(MSG_FATAL, "fscl_amd: permutation pool %s: %s", name, strerror(errno));
+    if (fd < 0 || ftruncate(fd, (off_t)p->map_bytes) != 0 || (err = posix_fallocate(fd, 0, (off_t)p->map_bytes)) != 0) {
+      logmsg(MSG_WARN, "fscl_amd: permutation pool %s (%zu MB): %s\n", name, p->map_bytes >> 20,
+             strerror(err ? err : errno));
+      fail = 1;
+      if (fd >= 0) { close(fd); shm_unlink(name); }
+    }
   }
-  if (fh_shm_barrier(m) != 0) logmsg(MSG_FATAL, "fscl_amd: permutation pool: rank exchange failed");
+  if (fh_shm_allgather_flags(m, &dummy, 1, 0, 0, 0, &fail) != 0)
+    logmsg(MSG_FATAL, "fscl_amd: permutation pool: rank exchange failed");
+  if (fail) { free(p); return NULL; }
   if (m->rank != 0) {
     struct stat sb;
     fd = shm_open(name, O_RDWR, 0600);

@@ -953,6 +953,14 @@ static void pool_setup(int n_snps, int K) {
       fh_pool_close(PL.pool);
     }
     PL.pool = fh_pool_open(D.shm, want);
+    PL.registered = 0;
+    if (!PL.pool) {  /* collective: every rank builds its own permutations this time */
+      PL.on = 0;
+      spec_start();
+      D.st.spec_threads = SP.n_th;
+      pb_reserve(n_snps, K);
+      return;
+    }
     PL.registered = fsclg_host_register(fh_pool_data(PL.pool), fh_pool_bytes(PL.pool)) == FSCLG_OK;
     if (!PL.registered)
       logmsg(MSG_WARN, "fscl_amd: the permutation pool could not be page-locked (%s): rows are copied to the "
