@@ -120,8 +120,10 @@ def profile_summary(args) -> tuple[dict | None, str | None]:
     def tag_order(q: Path):  # rNN then the revision letters: r02z < r02aa < r02ab
         tag = q.name.split("_")[0]
         return (tag[:3], len(tag), tag)
+    # a profile of this workload: rNN<rev>_<config>[chr<N>]_...summary.json (chr<N>: a --chromosomes job)
+    key = args.config.lower() + (f"chr{args.chromosomes}" if args.chromosomes else "")
     cands = [Path(args.profile_summary)] if args.profile_summary else sorted(
-        (ROOT / "profiles").glob(f"r*_{args.config.lower()}_*summary.json"), key=tag_order)
+        (ROOT / "profiles").glob(f"r*_{key}_*summary.json"), key=tag_order)
     for q in reversed(cands):
         try:
             d = json.loads(q.read_text())
@@ -353,7 +355,7 @@ def main() -> int:
             traffic = None
     mem = None
     mem_path = ROOT / "profiles" / "r03b_pmc_mem_c4_c2.json"
-    if mem_path.exists() and args.config.lower() in ("c4", "c2"):
+    if mem_path.exists() and args.config.lower() in ("c4", "c2") and not args.chromosomes:
         m = json.loads(mem_path.read_text())[args.config.lower()]
         t = m["totals_over_job"]
         mem = {"source": str(mem_path.relative_to(ROOT)), **{k: round(v, 3) for k, v in m["per_term"].items()},
