@@ -22,10 +22,14 @@ U=$(python3 -c "import sys; sys.path.insert(0, '$R'); import bench; print(bench.
 echo "usable CPUs: $U, W=$W"
 timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > /dev/null 2>&1  # warm caches
 FSCL_AMD_SIM=record:$REC timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w1_record.json 2> $OUT/w1_record.err || exit 1
-burn() {  # $1 spinning processes, each time-limited; their pids in BURN_PIDS
+burn() {  # $1 spinning processes (BURN=yield: spinning with sched_yield, as the ranks' exchange waits do
+          # after 4096 spins), each time-limited; their pids in BURN_PIDS
   BURN_PIDS=""
+  local code="while True: pass"
+  [ "${BURN:-spin}" = yield ] && code="import os
+while True: os.sched_yield()"
   for i in $(seq $1); do
-    timeout -k 5 600 python3 -c "while True: pass" &
+    timeout -k 5 600 python3 -c "$code" &
     BURN_PIDS="$BURN_PIDS $!"
   done
 }
@@ -42,11 +46,18 @@ SPEC_SINGLE=$((U - 1)); [ $SPEC_SINGLE -gt 32 ] && SPEC_SINGLE=32
 SPEC_REPL=$((U / W - 1)); [ $SPEC_REPL -lt 0 ] && SPEC_REPL=0
 SPEC_LEAD=$((U - W)); [ $SPEC_LEAD -lt 0 ] && SPEC_LEAD=0; [ $SPEC_LEAD -gt 32 ] && SPEC_LEAD=32
 BUSY_REPL=$(( (W - 1) * (SPEC_REPL + 1) ))
-for r in 1 2; do
-  run single $SPEC_SINGLE 0 $r
-  run replicated $SPEC_REPL $BUSY_REPL $r
-  run leader $SPEC_LEAD $((W - 1)) $r
-  # the split cells' speculative refine walks off
-  run leader_norefine $SPEC_LEAD $((W - 1)) $r FSCLG_SPEC_REFINE=0
+for r in $(seq ${ROUNDS:-2}); do
+  for v in ${VARIANTS:-single replicated leader leader_norefine}; do
+    case $v in
+      single) run single $SPEC_SINGLE 0 $r ;;
+      replicated) run replicated $SPEC_REPL $BUSY_REPL $r ;;
+      leader) run leader $SPEC_LEAD $((W - 1)) $r ;;
+      # the split cells' speculative refine walks off
+      leader_norefine) run leader_norefine $SPEC_LEAD $((W - 1)) $r FSCLG_SPEC_REFINE=0 ;;
+      # the leader oversubscribing: every CPU but its main thread, the other ranks' waits yielding
+      leader_all) run leader_all $SPEC_SINGLE $((W - 1)) $r ;;
+      single_norefine) run single_norefine $SPEC_SINGLE 0 $r FSCLG_SPEC_REFINE=0 ;;
+    esac
+  done
 done
 rm -f $REC
