@@ -3071,9 +3071,11 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
       }
       std::vector<int> lists[8];
       for (int u : B.order) lists[cls[u]].push_back(u);
-      // FSCLG_XCD_ORDER=1 (A/B): chromosome-major within a class -- an XCD then works on one of
-      // its chromosomes at a time (its L2 holds one site array instead of its run's 3 at C5)
-      static const int chr_major = getenv("FSCLG_XCD_ORDER") ? atoi(getenv("FSCLG_XCD_ORDER")) : 0;
+      // chromosome-major within a class (longest first within a chromosome): an XCD then works on
+      // one of its chromosomes at a time, so its L2 holds one site array instead of its run's
+      // three at C5 (measured, DESIGN.md §11.5: -1.1 % per C5 job, -0.6 % per C4 job;
+      // FSCLG_XCD_ORDER=0: longest first over the whole class, as before)
+      static const int chr_major = getenv("FSCLG_XCD_ORDER") ? atoi(getenv("FSCLG_XCD_ORDER")) : 1;
       if (chr_major)
         for (auto& l : lists)
           std::stable_sort(l.begin(), l.end(), [&](int x, int y) { return B.ucells[x].chr < B.ucells[y].chr; });
