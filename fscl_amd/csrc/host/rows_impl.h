@@ -13,7 +13,7 @@ static void ROW_CAT(chr_null_sums, ROW_SFX)(const ROW_T *row, double *out) {
   const int nl = D.chr_list ? D.n_chr_list : D.n_chr;
   int q, i;
   if (D.chr_list) for (q = 0; q < D.n_chr; q++) out[q] = 0.;
-#pragma omp parallel for schedule(dynamic, 1) private(i) if (nl > 1)
+#pragma omp parallel for schedule(dynamic, 1) private(i) if (nl > 1) num_threads(null_threads())
   for (q = 0; q < nl; q++) {
     const int c = D.chr_list ? D.chr_list[q] : q;
     double acc = 0.;

@@ -24,6 +24,8 @@
 #include <sys/time.h>
 #include <unistd.h>
 
+#include <omp.h>
+
 #include "fscl_host.h"
 
 #define CLR_NULL_DIST_SAVE 10000 /* scan-chromosome.c:227 */
@@ -483,6 +485,12 @@ static void prepare(scan_t *s, sm_ptable_t *sm) {
   D.tab_key = sm; D.snp_key = s->snps; D.n_snps_key = s->n_snps; D.key = key;
 }
 
+/* OpenMP threads of the main thread's whole-chromosome null sums (a speculation miss): with the
+   node leader's permutations the other ranks' main threads hold W - 1 of the usable CPUs, and
+   an OpenMP team larger than what is left spins in its barriers */
+static int g_null_nt = 0;
+static int null_threads(void) { return g_null_nt > 0 ? g_null_nt : omp_get_max_threads(); }
+
 /* the row-array routines at each staging width (rows_impl.h), and their dispatch on D.rb */
 #define ROW_T uint8_t
 #define ROW_SFX 8
@@ -780,7 +788,7 @@ static struct {
   const snp_t *snps;      /* the permutation's inputs (fixed while a job is posted) */
   int n;
   double nbp, width_mb;
-  pbuf_t pb[FSCLG_N_SLOTS + 2 * SPEC_MAX + 1];
+  pbuf_t pb[FSCLG_N_SLOTS + 3 * SPEC_MAX + 1];
   int n_pb, pb_cap, pb_nchr, pb_rb;
   int pb_in_pool;         /* the buffers are the leader's pool's (not owned here) */
 } SP = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
@@ -849,6 +857,7 @@ static int usable_cpus(void) {
    FSCL_AMD_PERM_LEADER=0 turns it off (every rank builds its own, as before). */
 static struct {
   int on;            /* in the current permute_pipelined call */
+  int sizing;        /* the leader's CPU sizing (on, or rank 0 of a rehearsal replay, FSCL_AMD_SIM) */
   fh_pool_t *pool;
   int registered;    /* this rank's devices read the pool directly (else: a copy into D.stage) */
 } PL;
@@ -858,15 +867,21 @@ static int perm_leader_wanted(void) {
   return D.world > 1 && D.shm && !D.sim && (!e || atoi(e) != 0);
 }
 
+/* the rehearsal (FSCL_AMD_SIM replay as rank 0 of world) sizes its threads as the leader would */
+static int perm_leader_sizing(void) {
+  const char *e = getenv("FSCL_AMD_PERM_LEADER");
+  return perm_leader_wanted() || (D.sim && D.sim_replay && D.world > 1 && D.rank == 0 && (!e || atoi(e) != 0));
+}
+
 /* worker threads: FSCL_AMD_SPEC, else this process's share of the usable CPUs (one process
    per GPU shares the node: LOCAL_WORLD_SIZE) less the main thread.  With the node leader's
    permutations: the leader takes every CPU the ranks' main threads leave, the others none */
 static int spec_threads_wanted(void) {
   const char *e = getenv("FSCL_AMD_SPEC"), *lw = getenv("LOCAL_WORLD_SIZE");
-  const int local = lw && atoi(lw) > 0 ? atoi(lw) : PL.on ? D.world : 1;
+  const int local = lw && atoi(lw) > 0 ? atoi(lw) : PL.sizing ? D.world : 1;
   int n;
   if (PL.on && D.rank != 0) return 0;
-  n = e ? atoi(e) : PL.on ? usable_cpus() - local : usable_cpus() / local - 1;
+  n = e ? atoi(e) : PL.sizing ? usable_cpus() - local : usable_cpus() / local - 1;
   return n < 0 ? 0 : n > SPEC_MAX ? SPEC_MAX : n;
 }
 
@@ -893,9 +908,18 @@ static void spec_stop(void) {
   SP.n_pb = SP.pb_cap = SP.pb_nchr = SP.pb_rb = SP.pb_in_pool = 0;
 }
 
+/* candidates posted per trial: two per worker thread (a C4 candidate takes ~0.7 ms of one
+   thread, a tail trial at 8 GPUs ~1.5-2.5 ms, so each thread builds two or three; the most
+   likely are posted first), at most SPEC_MAX */
+static int spec_ncand(void) { return SP.n_th * 2 < SPEC_MAX ? SP.n_th * 2 : SPEC_MAX; }
+
+/* buffers: K slots, the posted candidates, the cancelled ones still running (one per thread)
+   and the main thread's own (no job posted) */
+static int pb_count(int K) { return K + spec_ncand() + SP.n_th + 1; }
+
 /* buffers for K slots, the candidates and the main thread's own (no job posted) */
 static void pb_reserve(int n_snps, int K) {
-  const int want = K + 2 * SP.n_th + 1;
+  const int want = pb_count(K);
   int b;
   if (SP.pb_in_pool) { SP.n_pb = 0; SP.pb_in_pool = 0; SP.pb_cap = 0; }
   if (SP.pb_cap < n_snps || SP.pb_nchr < D.n_chr || SP.pb_rb != D.rb) {
@@ -941,7 +965,7 @@ static void slot_release(int slot) {
 static void pool_setup(int n_snps, int K) {
   const size_t rows = ((size_t)D.rb * (size_t)(n_snps ? n_snps : 1) + 4095) & ~(size_t)4095;
   const size_t nulb = ((sizeof(double) * (size_t)(D.n_chr ? D.n_chr : 1)) + 255) & ~(size_t)255;
-  const int nbuf = K + 2 * SP.n_th + 1;
+  const int nbuf = pb_count(K);
   const size_t want = (size_t)nbuf * (rows + nulb);
   unsigned f = D.rank == 0 && (!PL.pool || fh_pool_bytes(PL.pool) < want) ? 1u : 0u;
   char dummy = 0;
@@ -956,6 +980,8 @@ static void pool_setup(int n_snps, int K) {
     PL.registered = 0;
     if (!PL.pool) {  /* collective: every rank builds its own permutations this time */
       PL.on = 0;
+      PL.sizing = 0;
+      g_null_nt = 0;
       spec_start();
       D.st.spec_threads = SP.n_th;
       pb_reserve(n_snps, K);
@@ -1025,6 +1051,12 @@ static int spec_take(int d, fh_rand_t *g) {
   int c, hit = -1, bi = -1;
   pthread_mutex_lock(&SP.mu);
   for (c = 0; c < SP.n_job; c++) if (SP.d[c] == d) hit = c;
+  if (hit >= 0 && SP.state[hit] == 0) {
+    /* not started (the workers are still on likelier ones): building it here is faster than
+       waiting for a worker to get to it; the caller builds it (its buffer is freed below) */
+    D.st.spec_claimed++;
+    hit = -1;
+  }
   if (hit >= 0) {
     const double t0 = fh_now();
     while (SP.state[hit] < 2) pthread_cond_wait(&SP.done, &SP.mu);
@@ -1255,6 +1287,13 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   unsigned sig = 0;
   double *pnul;
   PL.on = perm_leader_wanted();
+  PL.sizing = perm_leader_sizing();
+  if (PL.sizing) {
+    const char *lw = getenv("LOCAL_WORLD_SIZE");
+    const int local = lw && atoi(lw) > 0 ? atoi(lw) : D.world;
+    g_null_nt = usable_cpus() - local + 1;
+    if (g_null_nt < 1) g_null_nt = 1;
+  }
   spec_start();
   D.st.spec_threads = SP.n_th;
   if (PL.on) pool_setup(s->n_snps, K);
@@ -1355,7 +1394,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     posted = SP.n_th > 0 && !(PL.on && D.rank != 0);  /* with the leader's permutations only the leader speculates */
     if (posted) {
       int dl[SPEC_MAX];
-      spec_post(g, dl, spec_candidates(s, pq, &A, SP.n_th, dl));
+      spec_post(g, dl, spec_candidates(s, pq, &A, spec_ncand(), dl));
     }
     draw_mark = g_draws;
     {
@@ -1427,6 +1466,8 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   for (k = 0; k < K; k++) slot_release(k);  /* every upload has read its buffer */
   spec_quiesce();
   PL.on = 0;
+  PL.sizing = 0;
+  g_null_nt = 0;
   if (tt) fclose(tt);
   tb_free(&A);
   for (k = 0; k < K; k++) { tb_free(&Bt[k]); free(nul[k]); }

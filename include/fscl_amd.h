@@ -230,6 +230,7 @@ typedef struct {
   unsigned long long spec_done; /* candidates completed (not cancelled) */
   double spec_gen_s;      /* worker seconds spent on the completed candidates */
   unsigned long long n_split_retry; /* fsclg_stats_t: split launches re-run unsplit */
+  unsigned long long spec_claimed;  /* chosen candidates not started yet, built by the main thread instead */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

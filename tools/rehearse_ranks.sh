@@ -34,29 +34,28 @@ while True: os.sched_yield()"
   done
 }
 unburn() { for p in $BURN_PIDS; do kill $p 2>/dev/null; done; wait $BURN_PIDS 2>/dev/null; BURN_PIDS=""; }
-run() {  # <name> <spec threads> <burners> <round> [env ...]
-  burn $3
-  env ${@:5} FSCL_AMD_SPEC=$2 FSCL_AMD_SIM=replay:$REC:$W:0 timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w${W}_$1_$4.json 2> $OUT/w${W}_$1_$4.err
+run() {  # <name> <burners> <round> [env ...]: the replay sizes its threads as the product would for that env
+  burn $2
+  env LOCAL_WORLD_SIZE=$W ${@:4} FSCL_AMD_SIM=replay:$REC:$W:0 timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w${W}_$1_$3.json 2> $OUT/w${W}_$1_$3.err
   local rc=$?
   unburn
   [ $rc -eq 0 ] || exit 1
-  echo "$1 (spec $2, $3 busy CPUs beside) round $4: $(python3 -c "import json;d=json.load(open('$OUT/w${W}_$1_$4.json'));s=d['stats'];print(round(d['ms_per_step']), 'ms/job; blocked on batches', round(s['wait_s'],3), 's; speculation', s['spec_hits'], '/', s['trials'], 'hits, wait', round(s['spec_wait_s'],3), 's')")"
+  echo "$1 ($2 busy CPUs beside; ${@:4}) round $3: $(python3 -c "import json;d=json.load(open('$OUT/w${W}_$1_$3.json'));s=d['stats'];print(round(d['ms_per_step']), 'ms/job; blocked on batches', round(s['wait_s'],3), 's; spec threads', s['spec_threads'], 'hits', s['spec_hits'], '/', s['trials'], 'claimed', s.get('spec_claimed'), 'wait', round(s['spec_wait_s'],3), 's; main-thread perm', round(s['host_perm_s'],3), 'null', round(s['host_null_s'],3), 's')")"
 }
-SPEC_SINGLE=$((U - 1)); [ $SPEC_SINGLE -gt 32 ] && SPEC_SINGLE=32
-SPEC_REPL=$((U / W - 1)); [ $SPEC_REPL -lt 0 ] && SPEC_REPL=0
-SPEC_LEAD=$((U - W)); [ $SPEC_LEAD -lt 0 ] && SPEC_LEAD=0; [ $SPEC_LEAD -gt 32 ] && SPEC_LEAD=32
-BUSY_REPL=$(( (W - 1) * (SPEC_REPL + 1) ))
+PER=$((U / W)); [ $PER -lt 1 ] && PER=1
 for r in $(seq ${ROUNDS:-2}); do
   for v in ${VARIANTS:-single replicated leader leader_norefine}; do
     case $v in
-      single) run single $SPEC_SINGLE 0 $r ;;
-      replicated) run replicated $SPEC_REPL $BUSY_REPL $r ;;
-      leader) run leader $SPEC_LEAD $((W - 1)) $r ;;
-      # the split cells' speculative refine walks off
-      leader_norefine) run leader_norefine $SPEC_LEAD $((W - 1)) $r FSCLG_SPEC_REFINE=0 ;;
-      # the leader oversubscribing: every CPU but its main thread, the other ranks' waits yielding
-      leader_all) run leader_all $SPEC_SINGLE $((W - 1)) $r ;;
-      single_norefine) run single_norefine $SPEC_SINGLE 0 $r FSCLG_SPEC_REFINE=0 ;;
+      # one process driving W GPUs: every spare CPU speculates for it, no other ranks
+      single) run single 0 $r LOCAL_WORLD_SIZE=1 FSCL_AMD_PERM_LEADER=0 ;;
+      # one process per GPU, each building its own permutations: the others' main + worker threads busy
+      replicated) run replicated $(( (W - 1) * PER )) $r FSCL_AMD_PERM_LEADER=0 ;;
+      # the node leader's permutations (the default): the others' main threads busy
+      leader) run leader $((W - 1)) $r ;;
+      leader_norefine) run leader_norefine $((W - 1)) $r FSCLG_SPEC_REFINE=0 ;;
+      single_norefine) run single_norefine 0 $r LOCAL_WORLD_SIZE=1 FSCL_AMD_PERM_LEADER=0 FSCLG_SPEC_REFINE=0 ;;
+      # the leader oversubscribing: a worker on every CPU but its main thread
+      leader_all) run leader_all $((W - 1)) $r FSCL_AMD_SPEC=$((U - 1)) ;;
     esac
   done
 done
