@@ -1,8 +1,14 @@
 set -o pipefail
 mkdir -p gpurun_out/r04c
 # does a rank's main thread burn a CPU while it waits for the GPU?  (FSCL_AMD_SPEC=0: no worker threads)
-FSCL_AMD_SPEC=0 /usr/bin/time -f "time_wall_user_sys %e %U %S" timeout -k 10 120 python3 bench.py --config C4 --steps 1 --warmup 0 --no-cpu-baseline --n-permute 200 > gpurun_out/r04c/cpuwait0.json 2> gpurun_out/r04c/cpuwait0.err || exit 1
-grep time_wall gpurun_out/r04c/cpuwait0.err; python3 -c "import json;d=json.load(open('gpurun_out/r04c/cpuwait0.json'));print('job s', d['ms_per_step']/1e3, 'setup s', d['setup_s'])"
+FSCL_AMD_SPEC=0 timeout -k 10 150 python3 -c "
+import resource, subprocess, sys, time
+t = time.time()
+r = subprocess.run([sys.executable, 'bench.py', '--config', 'C4', '--steps', '1', '--warmup', '0', '--no-cpu-baseline', '--n-permute', '200'], stdout=open('gpurun_out/r04c/cpuwait0.json', 'w'), stderr=open('gpurun_out/r04c/cpuwait0.err', 'w'))
+u = resource.getrusage(resource.RUSAGE_CHILDREN)
+print('time_wall_user_sys', round(time.time() - t, 2), u.ru_utime, u.ru_stime)
+sys.exit(r.returncode)" || exit 1
+python3 -c "import json;d=json.load(open('gpurun_out/r04c/cpuwait0.json'));print('job s', d['ms_per_step']/1e3, 'setup s', d['setup_s'])"
 BURN=spin VARIANTS="single replicated leader leader_norefine" ROUNDS=2 bash tools/rehearse_ranks.sh C4 r04c 8 || exit 1
 BURN=yield VARIANTS="leader leader_all" ROUNDS=1 bash tools/rehearse_ranks.sh C4 r04cy 8 || exit 1
 FSCL_AMD_LIBDIR=$PWD/fscl_amd/_build_rhot timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "matches_golden or full_size_configs or window_sum or (fixture and not C5_chr_p10000)" > gpurun_out/r04c/tests_hot.log 2>&1 || { echo HOT_TESTS_FAILED; tail -30 gpurun_out/r04c/tests_hot.log; exit 1; }
