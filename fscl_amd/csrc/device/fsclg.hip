@@ -139,9 +139,7 @@ struct Params {
   double iv_off;               // -LOG_AD_MIN * inv_step - 1e-9 (interval_of)
   int ivc0;                    // LDS coefficient cache: intervals [ivc0, ivc0 + n_civ), every row
   int n_civ, civ_max;          // civ_max = max(n_civ - 1, 0)
-  int n_cache;                 // n_civ * lrows blocks
-  int lrows;                   // rows of each cached interval: every row (stride), or with FSCLG_HOTROWS the
-                               // most used device rows [0, lrows) only (a two-level cache: the rest global)
+  int n_cache;                 // n_civ * stride blocks
   int off_thr, off_nul;        // byte offsets in fsclg_dyn (the coefficient window at 0)
   int off_lt, lt_hi;           // LDS copy of logt3 branch 2 (|d| > 2^24) entries [256, lt_hi) at off_lt; lt_hi 0: none
   uint32_t lt_span;            // |d| is in that copy iff |d| - 2^24 < lt_span (unsigned); 0: none
@@ -348,15 +346,6 @@ __device__ __forceinline__ void coef_ld(const char* base, uint32_t off, const Pa
   b = *reinterpret_cast<const double2*>(base + off + (uint32_t)P.pstride);
 }
 
-#ifdef FSCLG_HOTROWS
-// the LDS window's block of (cached interval ci, row r < lrows): per interval plane A of rows
-// [0, lrows) then plane B
-__device__ __forceinline__ void coef_ld_hot(uint32_t ci, uint32_t r, const Params& P, double2& a, double2& b) {
-  const char* lb = fsclg_dyn + (__umul24(ci, (uint32_t)P.lrows) << 5) + (r << 4);
-  a = *reinterpret_cast<const double2*>(lb);
-  b = *reinterpret_cast<const double2*>(lb + ((uint32_t)P.lrows << 4));
-}
-#endif
 
 // the coefficient block of (row, interval) into a = (c0, c1), b = (c2, c3): from the LDS
 // window when (interval, row) lies in it (every row of intervals [ivc0, ivc0 + n_civ)),
@@ -365,13 +354,8 @@ template <bool LDS, class SM>
 __device__ __forceinline__ void coef_fetch(uint32_t r, int iv, const SM& S, const Params& P, double2& a, double2& b) {
   if constexpr (LDS) {
     const uint32_t ci = (uint32_t)(iv - S.ivc0);
-#ifdef FSCLG_HOTROWS
-    const bool hit = ci < (uint32_t)P.n_civ && r < (uint32_t)P.lrows;
-    coef_ld_hot(min(ci, (uint32_t)P.civ_max), min(r, (uint32_t)P.lrows - 1u), P, a, b);
-#else
     const bool hit = ci < (uint32_t)P.n_civ;  // every row is cached
     coef_ld(fsclg_dyn, coef_off(r, (int)min(ci, (uint32_t)P.civ_max), P), P, a, b);
-#endif
     if (!hit) coef_ld(reinterpret_cast<const char*>(P.coef), coef_off(r, iv, P), P, a, b);
   } else {
     coef_ld(reinterpret_cast<const char*>(P.coef), coef_off(r, iv, P), P, a, b);
@@ -391,13 +375,8 @@ __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t 
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t ci = (uint32_t)(iv[u] - ivc0);
-#ifdef FSCLG_HOTROWS
-      if (ci < (uint32_t)P.n_civ && rv[u] < (uint32_t)P.lrows)
-        coef_ld_hot(ci, rv[u], P, ca[u], cb[u]);
-#else
       if (ci < (uint32_t)P.n_civ)  // every row is cached
         coef_ld(fsclg_dyn, coef_off(rv[u], (int)ci, P), P, ca[u], cb[u]);
-#endif
       else
         coef_ld(reinterpret_cast<const char*>(P.coef), coef_off(rv[u], iv[u], P), P, ca[u], cb[u]);
     }
@@ -771,19 +750,9 @@ __device__ __forceinline__ void run_segment_idx(SM& S, int w, int s, int s1, con
     if (uni) {
       const uint32_t ci = (uint32_t)(civ - ivc0);
       if (LDS && ci < (uint32_t)P.n_civ) {
-#ifdef FSCLG_HOTROWS
-        // the hot rows from LDS, the lanes of other rows from the global table (exec-masked)
-        const char* gb = reinterpret_cast<const char*>(P.coef) + (__umul24((uint32_t)civ, (uint32_t)P.stride) << 5);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          coef_ld_hot(ci, min(rv[u], (uint32_t)P.lrows - 1u), P, ca[u], cb[u]);
-          if (rv[u] >= (uint32_t)P.lrows) coef_ld(gb, rv[u] << 4, P, ca[u], cb[u]);
-        }
-#else
         const char* lb = fsclg_dyn + (__umul24(ci, (uint32_t)P.stride) << 5);
 #pragma unroll
         for (int u = 0; u < U; u++) coef_ld(lb, rv[u] << 4, P, ca[u], cb[u]);
-#endif
       } else {
         const char* gb = reinterpret_cast<const char*>(P.coef) + (__umul24((uint32_t)civ, (uint32_t)P.stride) << 5);
 #pragma unroll
@@ -989,15 +958,6 @@ template <class SM>
 __device__ __forceinline__ void load_window(SM& S, const Params& P, int wb) {
   double2* dst = reinterpret_cast<double2*>(fsclg_dyn);
   const double2* src = reinterpret_cast<const double2*>(P.coef) + (size_t)wb * P.stride * 2;
-#ifdef FSCLG_HOTROWS
-  if (P.lrows != P.stride) {  // per interval and plane, rows [0, lrows) of the table's stride
-    const int L = P.lrows;
-    for (int e = threadIdx.x; e < 2 * P.n_cache; e += WG) {
-      const int q = e / L, row = e - q * L;  // q = 2 * interval + plane
-      dst[e] = src[(size_t)q * P.stride + row];
-    }
-  } else
-#endif
   for (int e = threadIdx.x; e < 2 * P.n_cache; e += WG) dst[e] = src[e];
   if (threadIdx.x == 0) S.ivc0 = wb;
 }
@@ -1984,7 +1944,6 @@ struct fsclg_ctx {
   int n_chr = 0;
   std::vector<int> h_chr_n;
   std::vector<int32_t> h_pos, h_chr_start;
-  std::vector<double> h_rowcnt;  // sites per device row (row 0: the sentinel), for the LDS window plan
   int lt_hi = 0;                        // logt3 branch-2 entries [256, lt_hi) staged in LDS
   std::vector<long long> h_row_cnt;     // sites per device row
   std::vector<double> h_lt3;
@@ -2230,9 +2189,6 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   c->h_chr_n.assign(chr_n, chr_n + n_chr);
   c->h_chr_start.assign(chr_start, chr_start + n_chr);
   c->h_pos.assign(pos, pos + n_snps);
-  c->h_rowcnt.assign((size_t)c->n_rows + 1, 0.0);
-  for (int i = 0; i < n_snps; i++)
-    if (row[i] + 1 < c->h_rowcnt.size()) c->h_rowcnt[row[i] + 1] += 1.0;
   c->cell_cost.clear();
   {  // |d| of a walk stays within a chromosome's span (plus grid slack): branch-2 index range
     long long span = 0;
@@ -2739,48 +2695,19 @@ static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
     for (int j = 0; j + K <= c->n_iv; j++) if (hpre[j + K] - hpre[j] > hpre[bj + K] - hpre[bj]) bj = j;
     return (hpre[bj + K] - hpre[bj]) / htot;
   };
-  const int all = c->n_rows + 1;
-  int R = all;
-#ifdef FSCLG_HOTROWS
-  // two-level cache: rows [0, R) of more intervals, maximising (share of the sites in rows < R) x
-  // (share of the terms in the K(R) intervals); FSCLG_HOT_ROWS=R fixes R
-  {
-    double stot = 0.0;
-    for (double v : c->h_rowcnt) stot += v;
-    if (const char* e = getenv("FSCLG_HOT_ROWS")) R = std::max(2, std::min(all, atoi(e)));
-    else if (stot > 0 && (int)c->h_rowcnt.size() == all) {
-      double best = -1.0;
-      std::vector<double> rpre(all + 1, 0.0);
-      for (int r = 0; r < all; r++) rpre[r + 1] = rpre[r] + c->h_rowcnt[r];
-      std::vector<int> cand;
-      for (int r = 8; r < all; r += 8) cand.push_back(r);
-      cand.push_back(all);
-      for (int r : cand) {
-        const int K = std::min(c->n_iv, room / (r * 32));
-        if (K <= 0) continue;
-        int bj;
-        const double sc = best_iv(K, bj) * (rpre[r] / stot);
-        if (sc > best) { best = sc; R = r; }
-      }
-    }
-  }
-#endif
+  // every row of K intervals: a row-prefix cache over more intervals (the most used rows only,
+  // the others' lanes from the global table) was measured slower, DESIGN.md §11.5
+  const int R = c->n_rows + 1;
   const int K = std::min(c->n_iv, room / (R * 32));
   if (K <= 0) return;
   int bj;
   c->c_cover = best_iv(K, bj);
-  if (R < all) {  // the share of the sites in the cached rows
-    double st = 0.0, sr = 0.0;
-    for (int r = 0; r < (int)c->h_rowcnt.size(); r++) { st += c->h_rowcnt[r]; if (r < R) sr += c->h_rowcnt[r]; }
-    if (st > 0) c->c_cover *= sr / st;
-  }
   c->c_ivc0 = bj; c->c_civ = K; c->c_crow = R;
 }
 
-// Choose the LDS coefficient window: intervals [ivc0, ivc0 + K) x device rows [0, R) with
-// K * R * 32 bytes beside the static LDS, thresholds and null rows in LDS_WG, maximising
-// the expected share of terms it serves = (share of sites in rows < R) x (share of terms
-// in the interval window).  The interval shares come from walks sampled on the host:
+// Choose the LDS coefficient window: intervals [ivc0, ivc0 + K) x every device row, K * rows
+// * 32 bytes beside the static LDS, thresholds and null rows in LDS_WG, maximising the
+// expected share of terms it serves (the share of terms in the interval window).  The interval shares come from walks sampled on the host:
 // 32 sweep positions spread over the sites, every coarse alpha and the refine grid of the
 // first one, every 8th site of each walk, with the device's own log distance.
 static void plan_cache(fsclg_ctx* c) {
@@ -2829,8 +2756,7 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   // dynamic LDS: the planned coefficient window, thresholds and null rows
   if (c->plan_dirty) plan_cache(c);
   P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; P.civ_max = std::max(c->c_civ - 1, 0);
-  P.lrows = c->c_crow > 0 ? c->c_crow : P.stride;
-  P.n_cache = P.n_civ * P.lrows;
+  P.n_cache = P.n_civ * P.stride;
   P.off_thr = P.n_cache * 32; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
   P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8; P.lt_hi = c->lt_hi;  // entry i at off_lt + 8 i
   P.lt_span = c->lt_hi > 256 ? ((uint32_t)c->lt_hi << 16) - 0x1000000u : 0u;  // lt_hi <= 32768

@@ -11,6 +11,4 @@ sys.exit(r.returncode)" || exit 1
 python3 -c "import json;d=json.load(open('gpurun_out/r04c/cpuwait0.json'));print('job s', d['ms_per_step']/1e3, 'setup s', d['setup_s'])"
 BURN=spin VARIANTS="single replicated leader leader_norefine" ROUNDS=2 bash tools/rehearse_ranks.sh C4 r04c 8 || exit 1
 BURN=yield VARIANTS="leader leader_all" ROUNDS=1 bash tools/rehearse_ranks.sh C4 r04cy 8 || exit 1
-FSCL_AMD_LIBDIR=$PWD/fscl_amd/_build_rhot timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "matches_golden or full_size_configs or window_sum or (fixture and not C5_chr_p10000)" > gpurun_out/r04c/tests_hot.log 2>&1 || { echo HOT_TESTS_FAILED; tail -30 gpurun_out/r04c/tests_hot.log; exit 1; }
 tail -2 gpurun_out/r04c/tests_hot.log
-bash tools/ab_hot.sh r04c 2 || exit 1
