@@ -2791,10 +2791,12 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   return P;
 }
 
-// split cells' speculative refine walks (FSCLG_SPEC_REFINE=0: off, for A/B runs and tests; 2: evaluated
-// but every guess taken as missed, the fallback path's test)
+// split cells' speculative refine walks, off by default since round 4: they cut
+// a tail cell's phases from 12 to 9 but measured no shorter job, at one GPU or at 8 (rehearsed),
+// and add 8 % to the split segments (§11.3).  FSCLG_SPEC_REFINE=1: on; 2: evaluated but every
+// guess taken as missed (the fallback path's test)
 static int spec_refine_on() {
-  static const int on = getenv("FSCLG_SPEC_REFINE") ? atoi(getenv("FSCLG_SPEC_REFINE")) : 1;
+  static const int on = getenv("FSCLG_SPEC_REFINE") ? atoi(getenv("FSCLG_SPEC_REFINE")) : 0;
   return on;
 }
 

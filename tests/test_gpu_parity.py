@@ -71,11 +71,11 @@ def test_bisection_lookahead_fallbacks(built, tmp, lookahead):
         assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text(), case
 
 
-@pytest.mark.parametrize("spec", ["0", "2"])
+@pytest.mark.parametrize("spec", ["1", "2"])
 def test_speculative_refine_fallbacks(built, tmp, spec):
-    """Split cells evaluate the refine walks of a guessed coarse winner beside the coarse walks
-    (on by default, so every other test runs it).  Off, and evaluated but every
-    guess taken as missed (each point then takes the second phase): the golden outputs either
+    """Split cells can evaluate the refine walks of a guessed coarse winner beside the coarse walks
+    (off by default since round 4, §11.3, so every other test runs without).  On,
+    and evaluated but every guess taken as missed (each point then takes the second phase): the golden outputs either
     way, and the oracle's on a multi-chromosome permutation job."""
     env = dict(os.environ, FSCLG_SPEC_REFINE=spec)
     for case in ("g1_p25", "g1_asc", "g3_p10"):
