@@ -307,8 +307,10 @@ def test_two_ranks_on_one_gpu_match_one_rank(built, tmp, exchange):
         errs.append(err)
     assert (tmp / "o0.txt").read_text() == (GOLD / "g1_p25.out").read_text()
     assert not (tmp / "o1.txt").exists()  # one writer
-    if exchange == "shm":  # the leader's permutations: rank 1 builds none (no speculation threads)
+    if exchange == "shm":  # the leader's permutations: rank 1 builds none (no speculation threads),
         assert "spec_threads 0" in errs[1], errs[1][-400:]
+        # and both ranks' devices read the shared pool directly (page-locked, no copy)
+        assert not any("could not be page-locked" in e or "permutation pool" in e for e in errs), errs
 
 
 def test_pipelined_trials_match_lockstep_and_oracle(built, tmp, monkeypatch):
