@@ -54,6 +54,9 @@ for r in $(seq ${ROUNDS:-2}); do
       leader) run leader $((W - 1)) $r ;;
       leader_norefine) run leader_norefine $((W - 1)) $r FSCLG_SPEC_REFINE=0 ;;
       single_norefine) run single_norefine 0 $r LOCAL_WORLD_SIZE=1 FSCL_AMD_PERM_LEADER=0 FSCLG_SPEC_REFINE=0 ;;
+      # the leader with its per-trial trace (FSCL_AMD_TRIAL_TRACE: bulk wait, permutation, null sums +
+      # upload + cell lists, submit, blocking wait, flush, in microseconds per trial)
+      leader_trace) run leader_trace $((W - 1)) $r FSCL_AMD_TRIAL_TRACE=$OUT/trials_leader_$r.txt ;;
       # the leader oversubscribing: a worker on every CPU but its main thread
       leader_all) run leader_all $((W - 1)) $r FSCL_AMD_SPEC=$((U - 1)) ;;
     esac
