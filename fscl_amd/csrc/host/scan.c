@@ -987,8 +987,10 @@ static void pool_setup(int n_snps, int K) {
       pb_reserve(n_snps, K);
       return;
     }
-    PL.registered = fsclg_host_register(fh_pool_data(PL.pool), fh_pool_bytes(PL.pool)) == FSCLG_OK;
-    if (!PL.registered)
+    /* FSCL_AMD_POOL_COPY=1 (tests): the fallback taken when page-locking fails, on purpose */
+    PL.registered = !getenv("FSCL_AMD_POOL_COPY") &&
+                    fsclg_host_register(fh_pool_data(PL.pool), fh_pool_bytes(PL.pool)) == FSCLG_OK;
+    if (!PL.registered && !getenv("FSCL_AMD_POOL_COPY"))
       logmsg(MSG_WARN, "fscl_amd: the permutation pool could not be page-locked (%s): rows are copied to the "
                        "device staging\n", fsclg_last_error());
   }

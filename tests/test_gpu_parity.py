@@ -281,12 +281,13 @@ def test_search_maxalpha_dropin(built):
     assert t_pts < 1e-3 * len(rows)
 
 
-@pytest.mark.parametrize("exchange", ["callback", "shm", "shm_replicated"])
+@pytest.mark.parametrize("exchange", ["callback", "shm", "shm_replicated", "shm_copy"])
 def test_two_ranks_on_one_gpu_match_one_rank(built, tmp, exchange):
     """Parity mode with 2 processes (both on GPU 0): the exchange through a Python gloo
     callback, or the library's own shared-memory all-gather.  With the shared-memory exchange
     rank 0 builds every trial's permutation once into the node's shared pool and rank 1's device
-    reads it (FSCL_AMD_PERM_LEADER=0, "shm_replicated": each rank builds its own)."""
+    reads it (DESIGN.md §8; FSCL_AMD_PERM_LEADER=0, "shm_replicated": each rank builds its own;
+    "shm_copy": the pool's rows copied into each rank's own pinned staging, the fallback)."""
     c = manifest()["cases"]["g1_p25"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 1000), WORLD_SIZE="2",
                FSCL_AMD_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0", FSCL_AMD_RANK_TIMEOUT="120")
@@ -294,6 +295,8 @@ def test_two_ranks_on_one_gpu_match_one_rank(built, tmp, exchange):
         env["FSCL_MR_SHM"] = f"/fscl_amd_mr_{os.getpid()}"
     if exchange == "shm_replicated":
         env["FSCL_AMD_PERM_LEADER"] = "0"
+    if exchange == "shm_copy":  # the fallback when the pool cannot be page-locked: rows copied to own staging
+        env["FSCL_AMD_POOL_COPY"] = "1"
     procs = []
     for r in range(2):
         e = dict(env, RANK=str(r))
