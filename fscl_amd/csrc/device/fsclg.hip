@@ -1818,36 +1818,46 @@ window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nul
 // sums.  row == null: the uploaded rows (pr0).  T: the staging's row width (1, 2 or 4 bytes:
 // the narrowest that holds the table's rows, so that the PCIe reads are as few as can be).
 template <typename T>
-__global__ void __launch_bounds__(256) scatter_rows_kernel(uint2* __restrict__ pr, const T* __restrict__ row,
-                                                           const uint2* __restrict__ pr0, int n,
-                                                           double* __restrict__ chr_null,
-                                                           const double* __restrict__ chr_null_src, int n_chr) {
-  // a block takes 256 * E sites: one 16-B read of the pinned host rows per thread (PCIe reads
-  // few and wide; the staging is page-aligned) into an LDS tile, then each thread stores sites
-  // t, t + 256, ..., so that a wave's stores cover consecutive sites
+__global__ void __launch_bounds__(64) scatter_rows_kernel(uint2* __restrict__ pr, const T* __restrict__ row,
+                                                          const uint2* __restrict__ pr0, int n,
+                                                          double* __restrict__ chr_null,
+                                                          const double* __restrict__ chr_null_src, int n_chr) {
+  // One wave per block and no LDS, so that its blocks fit beside two resident search
+  // workgroups on a CU (they hold the whole LDS and 6 of the 8 wave slots per SIMD): an LDS-tiled
+  // version waited for search workgroups to retire, 137 us per C4 trial at ~7 GB/s, although the
+  // PCIe read itself takes ~30 us (tools/hostread_probe).  A block takes 64 * E
+  // sites: one 16-B read of the pinned host rows per lane (few, wide PCIe reads), then the wave
+  // transposes them by shuffles so that each store k covers 64 consecutive sites.
   constexpr int E = 16 / sizeof(T);
-  __shared__ __attribute__((aligned(16))) T tile[256 * E];
-  const int t = threadIdx.x, base = blockIdx.x * 256 * E;
+  const int l = threadIdx.x, base = blockIdx.x * 64 * E;
   if (row) {
-    const int i = base + E * t;
-    if (i + E <= n) *reinterpret_cast<uint4*>(&tile[E * t]) = *reinterpret_cast<const uint4*>(row + i);
+    union { uint4 v; T t[E]; } u;
+    u.v = make_uint4(0u, 0u, 0u, 0u);
+    const int i = base + E * l;
+    if (i + E <= n) u.v = *reinterpret_cast<const uint4*>(row + i);
     else
-      for (int k = 0; k < E; k++) if (i + k < n) tile[E * t + k] = row[i + k];
-    __syncthreads();
+      for (int k = 0; k < E; k++) if (i + k < n) u.t[k] = row[i + k];
+    // site base + 64 k + l sits in lane (64 k + l) / E, element l % E (E divides 64)
+    const int idx = l % E, dw = idx * (int)sizeof(T) / 4, sh = (idx * (int)sizeof(T) % 4) * 8;
 #pragma unroll
     for (int k = 0; k < E; k++) {
-      const int q = base + 256 * k + t;
-      if (q < n) pr[phys(q)].y = (uint32_t)tile[256 * k + t] + 1u;
+      const int src = (64 * k + l) / E;
+      const unsigned w0 = (unsigned)__shfl((int)u.v.x, src, 64), w1 = (unsigned)__shfl((int)u.v.y, src, 64);
+      const unsigned w2 = (unsigned)__shfl((int)u.v.z, src, 64), w3 = (unsigned)__shfl((int)u.v.w, src, 64);
+      const unsigned w = dw == 0 ? w0 : dw == 1 ? w1 : dw == 2 ? w2 : w3;
+      const unsigned r = sizeof(T) == 4 ? w : (w >> sh) & ((1u << (8 * sizeof(T))) - 1u);
+      const int q = base + 64 * k + l;
+      if (q < n) pr[phys(q)].y = r + 1u;
     }
   } else {
 #pragma unroll
     for (int k = 0; k < E; k++) {
-      const int q = base + 256 * k + t;
+      const int q = base + 64 * k + l;
       if (q < n) pr[phys(q)].y = pr0[phys(q)].y;
     }
   }
   if (blockIdx.x == 0 && chr_null_src)
-    for (int c = t; c < n_chr; c += 256) chr_null[c] = chr_null_src[c];
+    for (int c = l; c < n_chr; c += 64) chr_null[c] = chr_null_src[c];
 }
 
 }  // namespace
@@ -2262,7 +2272,7 @@ int fsclg_slot_set_rows(fsclg_ctx* c, int slot, const uint32_t* row, const doubl
     if (row != S.h_rows) memcpy(S.h_rows, row, sizeof(uint32_t) * c->n_snps);
   }
   if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
-  hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, dim3((c->n_snps + 1023) / 1024), dim3(256), 0, c->ustream,
+  hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, dim3((c->n_snps + 255) / 256), dim3(64), 0, c->ustream,
                      S.d_pr, row ? S.h_rows : nullptr, c->d_pr0, c->n_snps, S.d_chr_null,
                      chr_null ? S.h_null : nullptr, c->n_chr);
   HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
@@ -2332,16 +2342,16 @@ int fsclg_slot_set_rows_packed(fsclg_ctx* c, int slot, const void* row, int row_
   if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
   // read straight from the caller's portable pinned rows (one buffer can feed every device)
   const double* cn = chr_null ? S.h_null : nullptr;
-  const int per = 256 * (16 / row_bytes);  // sites per block
+  const int per = 64 * (16 / row_bytes);  // sites per block (one wave)
   const dim3 grid((c->n_snps + per - 1) / per);
   if (row_bytes == 1)
-    hipLaunchKernelGGL(scatter_rows_kernel<uint8_t>, grid, dim3(256), 0, c->ustream, S.d_pr,
+    hipLaunchKernelGGL(scatter_rows_kernel<uint8_t>, grid, dim3(64), 0, c->ustream, S.d_pr,
                        static_cast<const uint8_t*>(row), c->d_pr0, c->n_snps, S.d_chr_null, cn, c->n_chr);
   else if (row_bytes == 2)
-    hipLaunchKernelGGL(scatter_rows_kernel<uint16_t>, grid, dim3(256), 0, c->ustream, S.d_pr,
+    hipLaunchKernelGGL(scatter_rows_kernel<uint16_t>, grid, dim3(64), 0, c->ustream, S.d_pr,
                        static_cast<const uint16_t*>(row), c->d_pr0, c->n_snps, S.d_chr_null, cn, c->n_chr);
   else
-    hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, grid, dim3(256), 0, c->ustream, S.d_pr,
+    hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, grid, dim3(64), 0, c->ustream, S.d_pr,
                        static_cast<const uint32_t*>(row), c->d_pr0, c->n_snps, S.d_chr_null, cn, c->n_chr);
   HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
   HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
@@ -2358,7 +2368,7 @@ int fsclg_set_chr_null(fsclg_ctx* c, const double* chr_null) {
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");
   memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
   // the null sums only: a one-block scatter over no sites
-  hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, dim3(1), dim3(256), 0, c->ustream, S.d_pr, nullptr, c->d_pr0,
+  hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, dim3(1), dim3(64), 0, c->ustream, S.d_pr, nullptr, c->d_pr0,
                      0, S.d_chr_null, S.h_null, c->n_chr);
   HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
   HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
