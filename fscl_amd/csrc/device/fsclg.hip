@@ -1722,6 +1722,42 @@ __global__ void __launch_bounds__(256) chunk_table_kernel(const uint2* __restric
   tab[t] = ok ? make_double2((double)d0, (double)(d1 - d0)) : make_double2(nan, nan);
 }
 
+// Block maps.  Within one binade a chunk's increment depends on the running
+// integer m only through its parity (chunk_table_kernel: (d0, d1 - d0)), so the map of a run of
+// chunks is again m -> m + D[m & 1], and maps compose: the run [a, c) after [a, b) gives
+// D[p] = D1[p] + D2[(p + D1[p]) & 1].  chunk_tree_kernel composes the chunk table over aligned
+// blocks of 2^L chunks, L = 1 .. lmax, so that a window's interior takes O(log) steps instead of
+// one per chunk.  The partial sums are monotone (every null value <= 0), so a block keeps m in
+// its binade iff its end does, the same test as for one chunk.  Exactness: a block that can keep
+// any m in (-2^53, -2^52] inside has |D| < 2^53, an exact double; a larger |D| may round, but then
+// it is at least 2^53 in magnitude and fails the test anyway.  NaN (a positive, NaN or -inf null
+// value, or the padding past the last site) propagates through the composition.
+constexpr int CT_LMAX = 12;
+struct CTree {
+  const double2* p;              // level L >= 1, binade k, block b at p[off[L] + k * nb[L] + b]
+  int lmax;                      // 0: no blocks (one step per chunk, in groups of WCG)
+  int off[CT_LMAX + 1], nb[CT_LMAX + 1];
+};
+
+__device__ __forceinline__ double2 compose_maps(double2 f1, double2 f2) {
+  const double a0 = f1.x, a1 = f1.x + f1.y, b0 = f2.x, b1 = f2.x + f2.y;
+  const double D0 = a0 + ((((long long)a0) & 1ll) ? b1 : b0);       // entry parity 0
+  const double D1 = a1 + ((((long long)a1 + 1ll) & 1ll) ? b1 : b0);  // entry parity 1
+  return make_double2(D0, D1 - D0);
+}
+
+// one block per binade: levels 1 .. lmax in turn (level L from level L - 1, level 0 the chunk table)
+__global__ void __launch_bounds__(256) chunk_tree_kernel(const double2* __restrict__ ctab, int nstride, CTree T,
+                                                         double2* __restrict__ out) {
+  const int k = blockIdx.x;
+  for (int L = 1; L <= T.lmax; L++) {
+    const double2* prev = L == 1 ? ctab + (size_t)k * nstride : out + T.off[L - 1] + (size_t)k * T.nb[L - 1];
+    double2* cur = out + T.off[L] + (size_t)k * T.nb[L];
+    for (int b = threadIdx.x; b < T.nb[L]; b += 256) cur[b] = compose_maps(prev[2 * b], prev[2 * b + 1]);
+    __syncthreads();  // the level's writes before the next level reads them (one workgroup)
+  }
+}
+
 // A wave sums the windows of 64 consecutive starts (one per lane; 256 per block, tasks: [start,
 // count]), walking the absolute chunks in order, every lane at the same chunk:
 //  * interior groups: while every lane is at a whole chunk of its window, at least 2^emin in
@@ -1736,7 +1772,7 @@ __global__ void __launch_bounds__(256) chunk_table_kernel(const uint2* __restric
 __global__ void __launch_bounds__(WN_WG)
 window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nullrow,
                     const int2* __restrict__ tasks, int W, int emin, int ne, int nstride,
-                    const double2* __restrict__ tab, double* __restrict__ out) {
+                    const double2* __restrict__ tab, double* __restrict__ out, CTree T) {
   __builtin_amdgcn_s_setprio(2);  // beside the search kernels' waves, which wait on memory
   const int2 t = tasks[blockIdx.x];
   const int lane = threadIdx.x & 63;
@@ -1756,7 +1792,29 @@ window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nul
     if (c >= fast_lo && c < fast_hi) {  // uniform (c stays uniform: every branch that moves it is)
       const int e = (int)((__double_as_longlong(s) >> 52) & 0x7FF) - 1023;
       const int eu = __builtin_amdgcn_readfirstlane(e);
-      if (eu >= emin && eu < emin + ne && __builtin_amdgcn_ballot_w64(!(s < 0.0) || e != eu) == 0ull) {
+      if (eu >= emin && eu < emin + ne && __builtin_amdgcn_ballot_w64(!(s < 0.0) || e != eu) == 0ull &&
+          T.lmax > 0) {
+        // block steps: the largest aligned block at c that ends by fast_hi; on a binade crossing
+        // (or a NaN block) the same c with half the block, down to one chunk, then the general step
+        typedef const __attribute__((address_space(4))) double cdouble;
+        const double sc = __longlong_as_double((long long)(1023 + 52 - eu) << 52);   // 2^(52 - e)
+        const double isc = __longlong_as_double((long long)(1023 - 52 + eu) << 52);  // 2^(e - 52)
+        double m = s * sc;
+        int L = T.lmax;
+        while (c < fast_hi) {  // uniform
+          int Lc = min(L, 31 - __clz(fast_hi - c));
+          if (c) Lc = min(Lc, __ffs(c) - 1);
+          cdouble* tb = Lc == 0 ? (cdouble*)(tab + (size_t)(eu - emin) * nstride + c)
+                                : (cdouble*)(T.p + T.off[Lc] + (size_t)(eu - emin) * T.nb[Lc] + (c >> Lc));
+          const double d0 = tb[0], dd = tb[1];
+          const double mn = m + __builtin_fma((double)(__double2loint(m) & 1), dd, d0);
+          if (__builtin_amdgcn_ballot_w64(!(mn > -TWO53)) == 0ull) { m = mn; c += 1 << Lc; L = T.lmax; }
+          else if (Lc == 0) break;
+          else L = Lc - 1;
+        }
+        s = m * isc;
+        if (c >= fast_hi) continue;
+      } else if (eu >= emin && eu < emin + ne && __builtin_amdgcn_ballot_w64(!(s < 0.0) || e != eu) == 0ull) {
         const int gn = min(WCG, fast_hi - c);
         // uniform address, read-only for the kernel's life: through the constant address space, so
         // that the group's entries are scalar loads (registers shared by the wave; no texture path)
@@ -1886,6 +1944,9 @@ struct Slot {
   bool wpend = false;             // its time not yet added to window_ms (read without blocking later)
   int users = 0;                  // batches submitted on this slot and not yet waited for
   double2* d_ctab = nullptr;      // chunk_table_kernel's table for the slot's rows (window_chunk_kernel)
+  double2* d_ctree = nullptr;     // chunk_tree_kernel's block maps over it
+  size_t ctree_cap = 0;
+  CTree ctree = {};
   size_t ctab_cap = 0;            // entries
   bool ctab_valid = false;        // built for the slot's rows with (ctab_emin, ctab_ne)
   int ctab_emin = 0, ctab_ne = 0;
@@ -2094,7 +2155,8 @@ int fsclg_close(fsclg_ctx* c) {
                   c->d_stats, c->d_dfail};
   for (void* p : ptrs) if (p) hipFree(p);
   for (Slot& S : c->slot) {
-    for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null, (void*)S.d_ctab}) if (p) hipFree(p);
+    for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null, (void*)S.d_ctab, (void*)S.d_ctree})
+      if (p) hipFree(p);
     for (void* p : {(void*)S.h_rows, (void*)S.h_null, (void*)S.p_wtasks}) if (p) hipHostFree(p);
     hipEventDestroy(S.ready);
     if (S.wev0) hipEventDestroy(S.wev0);
@@ -2479,8 +2541,12 @@ static bool chunk_params(fsclg_ctx* c, long long W, int& emin, int& ne) {
 static int ctab_stride(const fsclg_ctx* c) { return (c->n_snps + WC - 1) / WC + WCG; }
 
 // the slot's chunk table (after its rows' upload, on the upload stream)
-static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne) {
-  if (S.ctab_valid && S.ctab_emin == emin && S.ctab_ne == ne) return FSCLG_OK;
+static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne, long long W) {
+  // block levels up to the window's length in chunks (FSCLG_WINDOW_TREE=0: none, one step per chunk)
+  static const int tree_on = getenv("FSCLG_WINDOW_TREE") ? atoi(getenv("FSCLG_WINDOW_TREE")) : 1;
+  int lmax = 0;
+  if (tree_on) while (lmax < CT_LMAX && (2ll << lmax) * WC <= W) lmax++;
+  if (S.ctab_valid && S.ctab_emin == emin && S.ctab_ne == ne && S.ctree.lmax == lmax) return FSCLG_OK;
   const int nstride = ctab_stride(c);
   const size_t need = (size_t)nstride * ne;
   if (S.ctab_cap < need) {
@@ -2493,6 +2559,27 @@ static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne) {
   hipLaunchKernelGGL(chunk_table_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, c->ustream, S.d_pr,
                      c->d_null, c->n_snps, emin, ne, nstride, S.d_ctab);
   HIPCHK(hipGetLastError(), "launch chunk_table_kernel");
+  S.ctree = CTree{};
+  S.ctree.lmax = lmax;
+  if (lmax > 0) {
+    const int nch = (c->n_snps + WC - 1) / WC;  // chunk indices with a table entry (the last may be NaN)
+    size_t tot = 0;
+    for (int L = 1; L <= lmax; L++) {
+      S.ctree.nb[L] = nch >> L;
+      S.ctree.off[L] = (int)tot;
+      tot += (size_t)ne * S.ctree.nb[L];
+    }
+    if (S.ctree_cap < tot) {
+      if (S.d_ctree) hipFree(S.d_ctree);
+      S.d_ctree = nullptr; S.ctree_cap = 0;
+      HIPCHK(hipMalloc((void**)&S.d_ctree, sizeof(double2) * (tot ? tot : 1)), "hipMalloc chunk tree");
+      S.ctree_cap = tot;
+    }
+    S.ctree.p = S.d_ctree;
+    hipLaunchKernelGGL(chunk_tree_kernel, dim3((unsigned)ne), dim3(256), 0, c->ustream, S.d_ctab, nstride, S.ctree,
+                       S.d_ctree);
+    HIPCHK(hipGetLastError(), "launch chunk_tree_kernel");
+  }
   S.ctab_valid = true; S.ctab_emin = emin; S.ctab_ne = ne;
   return FSCLG_OK;
 }
@@ -2554,9 +2641,9 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
     if ((r = window_time(c, S))) return r;  // the slot's previous launch (long finished)
     HIPCHK(hipEventRecord(S.wev0, c->ustream), "hipEventRecord");
     if (chunked) {
-      if ((r = ensure_ctab(c, S, emin, ne))) return r;
+      if ((r = ensure_ctab(c, S, emin, ne, W))) return r;
       hipLaunchKernelGGL(window_chunk_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
-                         c->d_wtasks, (int)W, emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null);
+                         c->d_wtasks, (int)W, emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null, S.ctree);
     } else {
       hipLaunchKernelGGL((window_null_kernel<WN_PER>), dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr,
                          c->d_null, c->d_wtasks, (int)W, S.d_win_null);
@@ -2631,9 +2718,9 @@ static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vect
   const int chunk_mode = getenv("FSCLG_WINDOW_CHUNK") ? atoi(getenv("FSCLG_WINDOW_CHUNK")) : 2;
   int emin = 0, ne = 0;
   if (chunk_mode >= 1 && chunk_params(c, 2ll * er + 1, emin, ne)) {
-    if ((r = ensure_ctab(c, S, emin, ne))) return r;
+    if ((r = ensure_ctab(c, S, emin, ne, 2ll * er + 1))) return r;
     hipLaunchKernelGGL(window_chunk_kernel, dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
-                       (int)(2ll * er + 1), emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null);
+                       (int)(2ll * er + 1), emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null, S.ctree);
   } else {
     hipLaunchKernelGGL((window_null_kernel<1>), dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
                        (int)(2ll * er + 1), S.d_win_null);

@@ -332,6 +332,102 @@ def _chunked_window_sum(v, W, a, emin, ne, C=64):
     return s
 
 
+def _tree_window_sum(v, W, a, emin, ne, C=64, lmax=11):
+    """Python restatement of the block steps of window_chunk_kernel (fsclg.hip):
+    the chunk maps m -> m + D[m & 1] of chunk_table_kernel composed over aligned blocks of 2^L
+    chunks (chunk_tree_kernel), and the running sum advanced by the largest aligned block that
+    keeps it in its binade, halving the block on a crossing; the rest as the chunked form."""
+    import math
+
+    def table(c, e):
+        vals = v[c * C:(c + 1) * C]
+        if len(vals) < C or any(not (x <= 0.0) or x == -math.inf for x in vals):
+            return None
+        u = math.ldexp(1.0, e - 52)
+        out = []
+        for p in (0, 1):
+            d, par = 0, p
+            for x in vals:
+                q = x / u
+                F = math.floor(q)
+                if q - F == 0.5:
+                    d += F + ((par + F) & 1)
+                    par = 0
+                else:
+                    R = round(q)
+                    d += R
+                    par = (par + R) & 1
+            out.append(d)
+        return out
+
+    def compose(f1, f2):  # f2 after f1: the block map for either entry parity
+        if f1 is None or f2 is None:
+            return None
+        return [f1[p] + f2[(p + f1[p]) & 1] for p in (0, 1)]
+
+    memo = {}
+
+    def block(L, b, e):  # the map of chunks [b 2^L, (b + 1) 2^L) in binade e
+        key = (L, b, e)
+        if key not in memo:
+            memo[key] = table(b, e) if L == 0 else compose(block(L - 1, 2 * b, e), block(L - 1, 2 * b + 1, e))
+        return memo[key]
+
+    s, i, end = 0.0, a, a + W
+    while i < end:  # head
+        if i % C == 0 and s <= -math.ldexp(1.0, emin):
+            break
+        s = s + v[i]
+        i += 1
+    L = lmax
+    while i + C <= end:  # whole chunks: aligned blocks
+        e = math.frexp(-s)[1] - 1 if s < 0.0 else None
+        c = i // C
+        if e is not None and emin <= e < emin + ne:
+            Lc = min(L, lmax, ((c & -c).bit_length() - 1) if c else lmax, ((end - i) // C).bit_length() - 1)
+            t = block(Lc, c >> Lc, e)
+            u = math.ldexp(1.0, e - 52)
+            m = int(s / u)
+            if t is not None and m + t[m & 1] > -(1 << 53):
+                s, i, L = (m + t[m & 1]) * u, i + (C << Lc), lmax
+                continue
+            if Lc > 0:
+                L = Lc - 1
+                continue
+        for j in range(C):  # the general step: chunk c site by site
+            s = s + v[i + j]
+        i += C
+        L = lmax
+    while i < end:
+        s = s + v[i]
+        i += 1
+    return s
+
+
+def test_block_window_sums_are_the_sequential_sums():
+    """The block steps of the window sums restated in Python: composing the
+    chunk maps over aligned blocks (their increment depends on the running sum only through its
+    parity, so they compose) and stepping by the largest block that stays in the binade gives
+    the sequential sum bit for bit, at every window offset, with ties, zeros, a positive value
+    and windows long enough for blocks of up to 2^5 chunks."""
+    import math
+    import random
+    rng = random.Random(13)
+    classes = [-rng.randint(1, 4000) / 64.0 if k % 3 == 0 else -rng.uniform(0.5, 60.0) for k in range(300)]
+    classes[5], classes[6] = 0.0, 3.5
+    v = [classes[rng.randrange(len(classes))] for _ in range(9000)]
+    v[4321] = 2.0  # a positive value: its chunk's blocks are invalid, that chunk site by site
+    mx = max(abs(x) for x in v)
+    W = 4100
+    emin = math.frexp(64 * mx)[1]
+    ne = math.frexp(W * mx)[1] - emin + 1
+    for a in list(range(0, 70, 3)) + list(range(70, len(v) - W + 1, 97)):
+        seq = 0.0
+        for i in range(a, a + W):
+            seq = seq + v[i]
+        assert _tree_window_sum(v, W, a, emin, ne, lmax=5).hex() == seq.hex(), a
+
+
 def test_chunked_window_sums_are_the_sequential_sums():
     """The chunked window null sums (fsclg.hip window_chunk_kernel) restated in
     Python: bit-identical to the sequential sum for windows at every offset, over null values
