@@ -1383,6 +1383,24 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       e->trial = trial; e->have = 0;
       pq[a].n++;
     }
+    /* a small bulk batch joins the blocking batch when the blocking batch's cells keep their full
+       split (8 members within the launch's 256-workgroup budget): the
+       early-prune tail's few bulk cells -- the most significant points, which never reach the
+       blocking class -- would otherwise run one workgroup per cell and hold up the host K trials
+       later.  Merged in ascending point order (the blocking batch's draws go in that order; the
+       merged points cannot draw).  The decision depends only on the counts: the same on every
+       rank.  FSCL_AMD_NO_MERGE=1: never. */
+    if (B->n > 0 && A.n + B->n <= 32 * D.world * D.n_dev && !getenv("FSCL_AMD_NO_MERGE")) {
+      int ia = A.n - 1, ib = B->n - 1, o = A.n + B->n - 1;
+      while (ib >= 0) {  /* merge from the back, in place in A (its capacity holds every active point) */
+        if (ia >= 0 && A.pt[ia] > B->pt[ib]) { A.pt[o] = A.pt[ia]; A.cells[o] = A.cells[ia]; ia--; }
+        else { A.pt[o] = B->pt[ib]; A.cells[o] = B->cells[ib]; ib--; }
+        o--;
+      }
+      D.st.n_merged += (unsigned long long)B->n;
+      A.n += B->n;
+      B->n = 0;
+    }
     D.st.n_crit += (unsigned long long)A.n;
     /* both batches always go through submit / wait (an empty share is a no-op), so that
        every rank takes part in the same exchanges */

@@ -231,6 +231,7 @@ typedef struct {
   double spec_gen_s;      /* worker seconds spent on the completed candidates */
   unsigned long long n_split_retry; /* fsclg_stats_t: split launches re-run unsplit */
   unsigned long long spec_claimed;  /* chosen candidates not started yet, built by the main thread instead */
+  unsigned long long n_merged;      /* scan_permute: bulk cells evaluated in their trial's blocking batch */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);
