@@ -444,7 +444,8 @@ def main() -> int:
                                      "cache_iv0", "cache_n_iv", "cache_n_rows", "cache_cover", "window_ms",
                                      "host_null_s", "host_upload_s", "search_s", "prune_s", "n_dup_cells",
                                      "n_ep_saved", "wait_s", "n_crit", "n_drain", "spec_threads", "spec_posted",
-                                     "spec_hits", "spec_cands", "spec_wait_s", "spec_done", "spec_gen_s")},
+                                     "spec_hits", "spec_cands", "spec_wait_s", "spec_done", "spec_gen_s",
+                                     "spec_claimed", "n_merged")},
     }
 
     # ---- parity of every timed job, whole job: initial scan + all permutation trials, their
