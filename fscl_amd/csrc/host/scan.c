@@ -1136,6 +1136,27 @@ static void tb_reserve(trial_batch_t *b, int n) {
 
 static void tb_free(trial_batch_t *b) { free(b->pt); free(b->cells); free(b->out); memset(b, 0, sizeof *b); }
 
+/* the most cells any device (of every rank) would get if batch B joined batch A: the devices'
+   shares are the cost-balanced contiguous split of tb_plan, over the merged ascending point list */
+static int merged_max_share(const scan_t *s, const trial_batch_t *A, const trial_batch_t *B, int eval_range) {
+  const int T = D.world * D.n_dev, n = A->n + B->n;
+  double *cost;
+  int ia = 0, ib = 0, k, g, mx = 0;
+  if (T <= 1) return n;
+  cost = fh_malloc(sizeof(double) * (size_t)n, "cost");
+  for (k = 0; k < n; k++) {
+    const int pt = (ib >= B->n || (ia < A->n && A->pt[ia] < B->pt[ib])) ? A->pt[ia++] : B->pt[ib++];
+    cost[k] = g_pcost && g_pcost[pt] > 0 ? g_pcost[pt] : window_cost(s->scan_pts[pt].chr, eval_range) / 32.0;
+  }
+  for (g = 0; g < T; g++) {
+    int lo, hi;
+    fscl_amd_partition(cost, n, g, T, &lo, &hi);
+    if (hi - lo > mx) mx = hi - lo;
+  }
+  free(cost);
+  return mx;
+}
+
 /* the local devices' shares of a batch, fixed at planning */
 static void tb_plan(trial_batch_t *b, int eval_range) {
   double *cost = NULL;
@@ -1390,7 +1411,8 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
        later.  Merged in ascending point order (the blocking batch's draws go in that order; the
        merged points cannot draw).  The decision depends only on the counts: the same on every
        rank.  FSCL_AMD_NO_MERGE=1: never. */
-    if (B->n > 0 && A.n + B->n <= 32 * D.world * D.n_dev && !getenv("FSCL_AMD_NO_MERGE")) {
+    if (B->n > 0 && A.n + B->n <= 32 * D.world * D.n_dev && !getenv("FSCL_AMD_NO_MERGE") &&
+        merged_max_share(s, &A, B, eval_range) <= 32) {
       int ia = A.n - 1, ib = B->n - 1, o = A.n + B->n - 1;
       while (ib >= 0) {  /* merge from the back, in place in A (its capacity holds every active point) */
         if (ia >= 0 && A.pt[ia] > B->pt[ib]) { A.pt[o] = A.pt[ia]; A.cells[o] = A.cells[ia]; ia--; }
