@@ -74,6 +74,9 @@ constexpr int SEG = FSCLG_SEG;     // terms per work segment
 #endif
 constexpr int SEG_SPLIT = FSCLG_SEG_SPLIT;  // split cells (latency): finer segments spread over the members' waves
 constexpr int MAXWALK = 32;        // 2 points x 16 candidates
+#ifndef FSCLG_MAXSPLIT
+#define FSCLG_MAXSPLIT 8  // members per split cell at most
+#endif
 constexpr int MAXWALK_SPLIT = 64;  // split cells: 2 points x (11 coarse + 15 speculative refine candidates)
 constexpr int MAXSEG_W = (163841 / SEG_SPLIT + 4 + 31) / 32 * 32;  // segments per walk (165 at 163841 terms, split;
                                                                   // each part's ends are 128-site aligned)
@@ -228,7 +231,7 @@ struct SmemT {
   int xbase;                      // split cells: this member's first tie slot
   int xfail;                      // split cells: PF_SPLIT_TIMEOUT if a member never arrived
   int iev;                        // FSCLG_INST_TRACE: events recorded so far
-  int xnt[8];                     // split cells: each member's tie count of the instance
+  int xnt[FSCLG_MAXSPLIT];        // split cells: each member's tie count of the instance
 };
 using Smem = SmemT<MAXWALK>;             // the throughput kernel (its LDS window takes the rest)
 using SmemSplit = SmemT<MAXWALK_SPLIT>;  // split cells: room for speculative refine walks (no LDS window)
@@ -254,7 +257,7 @@ using SmemSplit = SmemT<MAXWALK_SPLIT>;  // split cells: room for speculative re
 // segments' parity bits by XOR (each segment has one member), the fp64 sums of lanes past 2^51
 // in member order, the ties concatenated.  Two areas used in turn: a member writes instance
 // i + 2 only after every member has arrived at i + 1, i.e. has finished reading i.
-constexpr int MAXSPLIT = 8;
+constexpr int MAXSPLIT = FSCLG_MAXSPLIT;
 constexpr int XTIES = MAXTIES / MAXSPLIT;  // tie slots per member (more: the overflow path)
 struct XAcc {
   unsigned long long P[MAXSPLIT][MAXWALK_SPLIT], Q[MAXSPLIT][MAXWALK_SPLIT];
@@ -1903,7 +1906,7 @@ __global__ void __launch_bounds__(64) scatter_rows_kernel(uint2* __restrict__ pr
       const unsigned w0 = (unsigned)__shfl((int)u.v.x, src, 64), w1 = (unsigned)__shfl((int)u.v.y, src, 64);
       const unsigned w2 = (unsigned)__shfl((int)u.v.z, src, 64), w3 = (unsigned)__shfl((int)u.v.w, src, 64);
       const unsigned w = dw == 0 ? w0 : dw == 1 ? w1 : dw == 2 ? w2 : w3;
-      const unsigned r = sizeof(T) == 4 ? w : (w >> sh) & ((1u << (8 * sizeof(T))) - 1u);
+      const unsigned r = sizeof(T) == 4 ? w : (w >> sh) & (unsigned)((1ull << (8 * sizeof(T))) - 1ull);
       const int q = base + 64 * k + l;
       if (q < n) pr[phys(q)].y = r + 1u;
     }
