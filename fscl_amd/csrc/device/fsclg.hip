@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <unordered_map>
+#include <chrono>
 
 #include "../../../include/fsclg.h"
 
@@ -1927,6 +1928,14 @@ __global__ void __launch_bounds__(64) scatter_rows_kernel(uint2* __restrict__ pr
 constexpr int NSLOT = FSCLG_N_SLOTS;
 constexpr int NBATCH = FSCLG_N_BATCHES;
 
+// FSCLG_HOST_PROFILE=1 (development aid): host seconds in the shim's submit-side calls, printed to stderr at
+// fsclg_close: [0] fsclg_slot_windows, [1] waits for a slot's previous window launch, [2] fsclg_search_submit,
+// [3] its launches (the HIP calls), [4] its window check (ensure_windows)
+static double g_hprof[8];
+static double hnow() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+static bool hprof_on() { static const bool on = getenv("FSCLG_HOST_PROFILE") != nullptr; return on; }
+
+
 // one trial's rows on the device (fsclg_slot_set_rows): the (position, row) array, the
 // whole-chromosome null sums and the per-window null sums of those rows
 struct Slot {
@@ -2151,6 +2160,9 @@ int fsclg_open(int device, fsclg_ctx** out) {
 
 int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
+  if (hprof_on())
+    fprintf(stderr, "fsclg host profile: slot_windows %.3f s (window waits %.3f s), search_submit %.3f s "
+                    "(launches %.3f s, window check %.3f s)\n", g_hprof[0], g_hprof[1], g_hprof[2], g_hprof[3], g_hprof[4]);
   hipSetDevice(c->device);
   hipDeviceSynchronize();
   void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0,
@@ -2510,7 +2522,9 @@ static int ensure_io(Batch& B, int n) {
 // add a slot's pending window-kernel time to window_ms (blocks only if it is still running)
 static int window_time(fsclg_ctx* c, Slot& S) {
   if (!S.wpend) return FSCLG_OK;
+  const double t0 = hprof_on() ? hnow() : 0.0;
   HIPCHK(hipEventSynchronize(S.wev1), "hipEventSynchronize");
+  if (hprof_on()) g_hprof[1] += hnow() - t0;
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, S.wev0, S.wev1), "hipEventElapsedTime");
   c->window_ms += ms;
@@ -2703,7 +2717,11 @@ static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vect
   for (const int2& x : todo) blocks += (x.y - x.x + WN_WG - 1) / WN_WG;
   if (!blocks) return FSCLG_OK;
   // the slot's previous window launch has read its task list (launches on one stream, in order)
-  if (S.wpend) HIPCHK(hipEventSynchronize(S.wev1), "hipEventSynchronize");
+  if (S.wpend) {
+    const double t0 = hprof_on() ? hnow() : 0.0;
+    HIPCHK(hipEventSynchronize(S.wev1), "hipEventSynchronize");
+    if (hprof_on()) g_hprof[1] += hnow() - t0;
+  }
   if (S.wtask_cap < blocks) {
     if (S.p_wtasks) hipHostFree(S.p_wtasks);
     S.p_wtasks = nullptr; S.wtask_cap = 0;
@@ -2747,7 +2765,14 @@ static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vect
 // A trial's window null sums for the cells every batch on the slot will evaluate (all of them,
 // before the slot's first submit): only those windows when they are few (the pruned tail of a
 // long permutation test: a few hundred cells), every window otherwise.  One launch per trial.
+static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, int n_cells, int eval_range);
 int fsclg_slot_windows(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, int n_cells, int eval_range) {
+  const double t0 = hprof_on() ? hnow() : 0.0;
+  const int r = slot_windows_impl(c, slot, cells, n_cells, eval_range);
+  if (hprof_on()) g_hprof[0] += hnow() - t0;
+  return r;
+}
+static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, int n_cells, int eval_range) {
   if (!c || slot < 0 || slot >= NSLOT || (!cells && n_cells) || n_cells < 0 || eval_range < 0)
     return set_err(FSCLG_E_ARG, "slot windows");
   if (!c->d_pr0) return set_err(FSCLG_E_STATE, "snps not uploaded");
@@ -2914,7 +2939,14 @@ static void note_alphas(fsclg_ctx* c, const fsclg_point_t* out, int n) {
 }
 
 // one launch of search_maxpos_kernel with n blocks on the batch's stream (events recorded by the caller)
+static int launch_blocks_impl(hipStream_t stream, const Params& P, int n);
 static int launch_blocks(hipStream_t stream, const Params& P, int n) {
+  const double t0 = hprof_on() ? hnow() : 0.0;
+  const int r = launch_blocks_impl(stream, P, n);
+  if (hprof_on()) g_hprof[3] += hnow() - t0;
+  return r;
+}
+static int launch_blocks_impl(hipStream_t stream, const Params& P, int n) {
   const int grid = n;
   const int dyn = P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
   const int stat_m = (int)((sizeof(Smem) + 15) / 16 * 16), stat_s = (int)((sizeof(SmemSplit) + 15) / 16 * 16);
@@ -2966,8 +2998,17 @@ static unsigned long long cell_key(const fsclg_cell_t& x) {
          (unsigned long long)(uint32_t)x.end_pos;
 }
 
+static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* cells, int n_cells,
+                              int eval_range, int bp_resl);
 int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* cells, int n_cells, int eval_range,
                         int bp_resl) {
+  const double t0 = hprof_on() ? hnow() : 0.0;
+  const int r = search_submit_impl(c, batch, slot, cells, n_cells, eval_range, bp_resl);
+  if (hprof_on()) g_hprof[2] += hnow() - t0;
+  return r;
+}
+static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* cells, int n_cells,
+                              int eval_range, int bp_resl) {
   if (!c || (!cells && n_cells) || n_cells < 0) return set_err(FSCLG_E_ARG, "cells");
   if (batch < 0 || batch >= NBATCH || slot < 0 || slot >= NSLOT) return set_err(FSCLG_E_ARG, "batch/slot");
   if (!c->d_pr0 || !c->d_coef || !c->d_la_coarse) return set_err(FSCLG_E_STATE, "tables/snps/alpha grid not set");
@@ -2989,7 +3030,11 @@ int fsclg_search_submit(fsclg_ctx* c, int batch, int slot, const fsclg_cell_t* c
     c->slot[slot].users++;
     return FSCLG_OK;
   }
-  if ((r = ensure_windows(c, slot, eval_range, cells, n_cells))) return r;
+  {
+    const double t0 = hprof_on() ? hnow() : 0.0;
+    if ((r = ensure_windows(c, slot, eval_range, cells, n_cells))) return r;
+    if (hprof_on()) g_hprof[4] += hnow() - t0;
+  }
   // identical cells are evaluated once (permutation cells are G-aligned, so two points can
   // share one), and so is an endpoint shared by neighbouring cells (scan-chromosome.c:130-134
   // evaluates both ends of every cell): a first launch evaluates the distinct endpoints, the
