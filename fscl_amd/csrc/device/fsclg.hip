@@ -1931,7 +1931,7 @@ constexpr int NBATCH = FSCLG_N_BATCHES;
 // FSCLG_HOST_PROFILE=1 (development aid): host seconds in the shim's submit-side calls, printed to stderr at
 // fsclg_close: [0] fsclg_slot_windows, [1] waits for a slot's previous window launch, [2] fsclg_search_submit,
 // [3] its launches (the HIP calls), [4] its window check (ensure_windows)
-static double g_hprof[8];
+static double g_hprof[12];
 static double hnow() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 static bool hprof_on() { static const bool on = getenv("FSCLG_HOST_PROFILE") != nullptr; return on; }
 
@@ -2161,8 +2161,10 @@ int fsclg_open(int device, fsclg_ctx** out) {
 int fsclg_close(fsclg_ctx* c) {
   if (!c) return FSCLG_OK;
   if (hprof_on())
-    fprintf(stderr, "fsclg host profile: slot_windows %.3f s (window waits %.3f s), search_submit %.3f s "
-                    "(launches %.3f s, window check %.3f s)\n", g_hprof[0], g_hprof[1], g_hprof[2], g_hprof[3], g_hprof[4]);
+    fprintf(stderr, "fsclg host profile: slot_windows %.3f s (window waits %.3f s, ranges %.3f s, partial launch "
+                    "%.3f s), search_submit %.3f s (launches %.3f s, window check %.3f s, dedup + endpoints %.3f s, "
+                    "order %.3f s)\n", g_hprof[0], g_hprof[1], g_hprof[5], g_hprof[6], g_hprof[2], g_hprof[3], g_hprof[4],
+            g_hprof[7], g_hprof[8]);
   hipSetDevice(c->device);
   hipDeviceSynchronize();
   void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0,
@@ -2788,7 +2790,9 @@ static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, 
     if (c->h_chr_n[ch] > W) all += (c->h_chr_n[ch] - W + 1 + WW - 1) / WW;
   if (!all) return FSCLG_OK;  // no chromosome above the window: the whole-chromosome sums serve
   std::vector<int2> need;
+  const double t0 = hprof_on() ? hnow() : 0.0;
   window_ranges(c, eval_range, cells, n_cells, need);
+  if (hprof_on()) g_hprof[5] += hnow() - t0;
   long long waves = 0;
   for (const int2& x : need) waves += (x.y - x.x + WW - 1) / WW;
   if (2 * waves >= all) {  // most windows: every one, the dense kernel's way
@@ -2797,7 +2801,10 @@ static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, 
   }
   S.wdone.clear();
   S.win_valid = false;
-  return launch_partial_windows(c, S, eval_range, need);
+  const double t1 = hprof_on() ? hnow() : 0.0;
+  const int r = launch_partial_windows(c, S, eval_range, need);
+  if (hprof_on()) g_hprof[6] += hnow() - t1;
+  return r;
 }
 
 
@@ -3035,6 +3042,7 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
     if ((r = ensure_windows(c, slot, eval_range, cells, n_cells))) return r;
     if (hprof_on()) g_hprof[4] += hnow() - t0;
   }
+  const double t_dd = hprof_on() ? hnow() : 0.0;
   // identical cells are evaluated once (permutation cells are G-aligned, so two points can
   // share one), and so is an endpoint shared by neighbouring cells (scan-chromosome.c:130-134
   // evaluates both ends of every cell): a first launch evaluates the distinct endpoints, the
@@ -3102,6 +3110,8 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
       for (int u = 0; u < nu; u++) B.ucell_ep[u] = make_int2(to[B.ucell_ep[u].x], to[B.ucell_ep[u].y]);
     }
   }
+  if (hprof_on()) g_hprof[7] += hnow() - t_dd;
+  const double t_or = hprof_on() ? hnow() : 0.0;
   // longest first: each cell's cost in its last launch (permutation trials repeat the cells),
   // else a guess (cells nearer the middle of a chromosome walk further on both sides)
   std::vector<double> cost(nu);
@@ -3161,6 +3171,7 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
       nl = (int)(8 * L);
     }
   }
+  if (hprof_on()) g_hprof[8] += hnow() - t_or;
   if ((r = ensure_io(B, nl))) return r;
   if (use_ep) {
     if ((r = ensure_buf(&B.d_ept, &B.ept_cap, ne))) return r;
