@@ -1944,6 +1944,7 @@ struct Slot {
   double* d_win_null = nullptr;   // [n_snps], valid for (win_er, rows) while win_valid
   int win_er = -1;
   bool win_valid = false;         // win_null holds every window start, or (win_part) the ranges wdone
+  bool win_fresh = false;         // fsclg_slot_windows covered every cell the slot's next batches submit
   bool win_part = false;
   std::vector<int2> wdone;        // window starts [x, y) summed for the slot's rows, sorted, disjoint
   int2* p_wtasks = nullptr;       // pinned: the tasks of the slot's last partial window launch
@@ -2244,7 +2245,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->ustream))) return r;
   c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
   c->plan_dirty = true;
-  for (Slot& S : c->slot) { S.win_valid = false; S.ctab_valid = false; }
+  for (Slot& S : c->slot) { S.win_valid = false; S.ctab_valid = false; S.win_fresh = false; }
   return FSCLG_OK;
 }
 
@@ -2267,7 +2268,7 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
     if ((r = upload(&S.d_pr, pr.data(), pr.size(), c->ustream))) return r;
     if ((r = upload<double>(&S.d_chr_null, nullptr, (size_t)n_chr, c->ustream))) return r;
     if ((r = upload<double>(&S.d_win_null, nullptr, (size_t)n_snps, c->ustream))) return r;
-    S.win_valid = false; S.win_er = -1; S.ctab_valid = false;
+    S.win_valid = false; S.win_er = -1; S.ctab_valid = false; S.win_fresh = false;
     HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   }
   c->n_snps = n_snps;
@@ -2343,7 +2344,7 @@ int fsclg_slot_set_rows(fsclg_ctx* c, int slot, const uint32_t* row, const doubl
   int r;
   if ((r = ensure_row_staging(c, S))) return r;
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read the staging
-  S.win_valid = false; S.ctab_valid = false;
+  S.win_valid = false; S.ctab_valid = false; S.win_fresh = false;
   if (row) {
     uint32_t mx = 0;
     for (int i = 0; i < c->n_snps; i++) mx = row[i] > mx ? row[i] : mx;  // vectorised validation
@@ -2417,7 +2418,7 @@ int fsclg_slot_set_rows_packed(fsclg_ctx* c, int slot, const void* row, int row_
   int r;
   if ((r = ensure_null_staging(c, S))) return r;
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read h_null
-  S.win_valid = false; S.ctab_valid = false;
+  S.win_valid = false; S.ctab_valid = false; S.win_fresh = false;
   if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
   // read straight from the caller's portable pinned rows (one buffer can feed every device)
   const double* cn = chr_null ? S.h_null : nullptr;
@@ -2771,6 +2772,9 @@ static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, 
 int fsclg_slot_windows(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, int n_cells, int eval_range) {
   const double t0 = hprof_on() ? hnow() : 0.0;
   const int r = slot_windows_impl(c, slot, cells, n_cells, eval_range);
+  // the caller's promise (fsclg.h): the slot's batches until its next rows submit only these cells, so
+  // their submits need not check the windows again
+  if (r == FSCLG_OK && slot >= 0 && slot < NSLOT) c->slot[slot].win_fresh = true;
   if (hprof_on()) g_hprof[0] += hnow() - t0;
   return r;
 }
@@ -3039,7 +3043,9 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
   }
   {
     const double t0 = hprof_on() ? hnow() : 0.0;
-    if ((r = ensure_windows(c, slot, eval_range, cells, n_cells))) return r;
+    const Slot& S = c->slot[slot];
+    if (!(S.win_fresh && S.win_valid && S.win_er == eval_range))
+      if ((r = ensure_windows(c, slot, eval_range, cells, n_cells))) return r;
     if (hprof_on()) g_hprof[4] += hnow() - t0;
   }
   const double t_dd = hprof_on() ? hnow() : 0.0;
