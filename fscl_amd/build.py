@@ -65,8 +65,8 @@ def build_native(force: bool = False, trace: bool = False, variant: str | None =
 
 def _build_native(force: bool, trace: bool, defines: tuple[str, ...] = ()) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
-    # every header a source may include (csrc/host/*.h: fscl_host.h, rows_impl.h, ...) and this file (the flags)
-    hdrs = list((ROOT / "include").glob("*.h")) + sorted((CSRC / "host").glob("*.h")) + [Path(__file__)]
+    # every header a source may include (csrc/host/*.h: fscl_host.h, rows_impl.h, ...; csrc/device/*.h) and this file (the flags)
+    hdrs = list((ROOT / "include").glob("*.h")) + sorted((CSRC / "host").glob("*.h")) + sorted((CSRC / "device").glob("*.h")) + [Path(__file__)]
     objs = []
     for src in HOST_SRC:
         s = CSRC / "host" / src

@@ -41,6 +41,7 @@
 #include <chrono>
 
 #include "../../../include/fsclg.h"
+#include "cell_order.h"
 
 #pragma clang fp contract(off)
 
@@ -2684,49 +2685,6 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
 // [start, end] has its nearest SNP in [j(start) - 1, j(end)], search_snppos's j being the least
 // index in [1, n) with position >= pos (n if none), and the window start is monotone in the
 // nearest SNP), merged, for the chromosomes above 2*er+1 SNPs
-static bool same_cell(const fsclg_cell_t& a, const fsclg_cell_t& b) {
-  return a.chr == b.chr && a.start_pos == b.start_pos && a.end_pos == b.end_pos;
-}
-
-extern "C++" {
-// sort idx by less: a linear pass when it is already in order, a merge when it is two ascending
-// runs (the host's classes of cells), a sort otherwise
-template <class Less>
-static void sort_runs(std::vector<int>& idx, Less less) {
-  const size_t n = idx.size();
-  size_t k = 1;
-  while (k < n && !less(idx[k], idx[k - 1])) k++;
-  if (k >= n) return;
-  size_t m = k + 1;
-  while (m < n && !less(idx[m], idx[m - 1])) m++;
-  if (m >= n) std::inplace_merge(idx.begin(), idx.begin() + k, idx.end(), less);
-  else std::stable_sort(idx.begin(), idx.end(), less);
-}
-}
-
-// lower_bound(pos + 1, pos + n, x) - pos, galloping out from h in [1, n], an earlier answer
-static int lower_bound_from(const int32_t* pos, int n, int h, int x) {
-  int lo, hi;  // every j < lo has pos[j] < x; pos[hi] >= x or hi == n
-  if (h < n && pos[h] < x) {
-    lo = h + 1; hi = n;
-    for (int s = 1;; s <<= 1) {
-      const long long t = (long long)h + s;
-      if (t >= n) break;
-      if (pos[t] >= x) { hi = (int)t; break; }
-      lo = (int)t + 1;
-    }
-  } else {
-    lo = 1; hi = h;
-    for (int s = 1;; s <<= 1) {
-      const long long t = (long long)h - s;
-      if (t < 1) break;
-      if (pos[t] < x) { lo = (int)t + 1; break; }
-      hi = (int)t;
-    }
-  }
-  return (int)(std::lower_bound(pos + lo, pos + hi, x) - pos);
-}
-
 static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out) {
   const long long W = 2ll * er + 1;
   std::vector<int2> need;
@@ -2740,7 +2698,7 @@ static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_
     const int cs = c->h_chr_start[ch], ce = cs + (int)n - 1;
     const int32_t* pos = c->h_pos.data() + cs;
     if (ch != hint_chr) { hint_chr = ch; hint = 1; }
-    auto jof = [&](int x) { return hint = lower_bound_from(pos, (int)n, hint, x); };
+    auto jof = [&](int x) { return hint = cellorder::lower_bound_from(pos, (int)n, hint, x); };
     const int nlo = std::max(jof(cells[i].start_pos) - 1, 0), nhi = std::min(jof(cells[i].end_pos), (int)n - 1);
     auto wsof = [&](int nl) {
       const int near = cs + nl;
@@ -2752,7 +2710,7 @@ static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_
   }
   std::vector<int> idx(need.size());
   for (size_t k = 0; k < need.size(); k++) idx[k] = (int)k;
-  sort_runs(idx, [&need](int a, int b) { return need[a].x < need[b].x; });
+  cellorder::sort_runs(idx, [&need](int a, int b) { return need[a].x < need[b].x; });
   out.clear();
   for (int k : idx) {
     const int2& x = need[k];
@@ -3102,62 +3060,11 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
   // share one), and so is an endpoint shared by neighbouring cells (scan-chromosome.c:130-134
   // evaluates both ends of every cell): a first launch evaluates the distinct endpoints, the
   // cell launch reads them.  Same inputs, same device arithmetic: identical results.
-  // Both by exact comparison in (chromosome, position) order, not hashing: the host submits
-  // its points in that order (one run per class of cells, each ascending), so the order is a
-  // linear check or a merge of the runs, and equal cells and shared endpoints are neighbours.
-  auto cless = [cells](int a, int b) {
-    const fsclg_cell_t &x = cells[a], &y = cells[b];
-    return x.chr != y.chr ? x.chr < y.chr : x.start_pos != y.start_pos ? x.start_pos < y.start_pos : x.end_pos < y.end_pos;
-  };
-  B.sidx.resize(n_cells);
-  for (int i = 0; i < n_cells; i++) B.sidx[i] = i;
-  sort_runs(B.sidx, cless);
-  B.ucells.clear();
-  B.uidx.resize(n_cells);
-  for (int k = 0; k < n_cells; k++) {
-    const fsclg_cell_t& x = cells[B.sidx[k]];
-    if (B.ucells.empty() || !same_cell(B.ucells.back(), x)) B.ucells.push_back(x);
-    B.uidx[B.sidx[k]] = (int)B.ucells.size() - 1;
-  }
+  // Both by exact comparison in (chromosome, position) order, not hashing (cell_order.h)
+  cellorder::dedup_cells(cells, n_cells, B.sidx, B.ucells, B.uidx);
   const int nu = (int)B.ucells.size();
   c->n_dup_cells += (unsigned long long)(n_cells - nu);
-  // endpoints 2u (start) and 2u + 1 (end); the starts are in order, and the ends too unless cells nest
-  auto ekey = [](int chr, int pos) {  // order-preserving for signed positions
-    return ((unsigned long long)(uint32_t)chr << 32) | (uint32_t)(pos ^ (int)0x80000000);
-  };
-  B.ekeys.resize(2 * nu);
-  for (int u = 0; u < nu; u++) {
-    B.ekeys[2 * u] = ekey(B.ucells[u].chr, B.ucells[u].start_pos);
-    B.ekeys[2 * u + 1] = ekey(B.ucells[u].chr, B.ucells[u].end_pos);
-  }
-  B.sidx.resize(2 * nu);
-  {
-    bool ends_sorted = true;
-    for (int u = 1; u < nu && ends_sorted; u++) ends_sorted = B.ekeys[2 * u + 1] >= B.ekeys[2 * u - 1];
-    auto eless = [&B](int a, int b) { return B.ekeys[a] < B.ekeys[b] || (B.ekeys[a] == B.ekeys[b] && a < b); };
-    if (ends_sorted) {  // merge the two ascending sequences
-      int i = 0, j = 0, k = 0;
-      while (i < nu || j < nu) {
-        if (j >= nu || (i < nu && !eless(2 * j + 1, 2 * i))) B.sidx[k++] = 2 * i++;
-        else B.sidx[k++] = 2 * j++ + 1;
-      }
-    } else {
-      for (int e = 0; e < 2 * nu; e++) B.sidx[e] = e;
-      std::sort(B.sidx.begin(), B.sidx.end(), eless);
-    }
-  }
-  B.epos.clear();
-  B.ucell_ep.resize(nu);
-  unsigned long long lastk = 0;
-  for (int k = 0; k < 2 * nu; k++) {
-    const int e = B.sidx[k], u = e >> 1;
-    if (B.epos.empty() || B.ekeys[e] != lastk) {
-      B.epos.push_back(make_int2(B.ucells[u].chr, (e & 1) ? B.ucells[u].end_pos : B.ucells[u].start_pos));
-      lastk = B.ekeys[e];
-    }
-    if (e & 1) B.ucell_ep[u].y = (int)B.epos.size() - 1;
-    else B.ucell_ep[u].x = (int)B.epos.size() - 1;
-  }
+  cellorder::dedup_endpoints(B.ucells, B.ekeys, B.sidx, B.epos, B.ucell_ep);
   const int ne = (int)B.epos.size();
   // split cells: a batch of few cells (the permutation pipeline's blocking batch in the
   // pruned tail) gives each cell up to split_max workgroups, within a budget of workgroups

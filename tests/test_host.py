@@ -473,3 +473,16 @@ def test_c3_input_is_ascertained_and_its_fixture_is_not_degenerate():
     assert all(float.fromhex(r[2]) != 0.0 for r in rows)
     assert fx["sum_permute_n"] > 21 * fx["n_points"]
     assert max(int(r[10]) for r in rows) > 21
+
+
+def test_cell_order_dedup_and_search(tmp_path):
+    """The submit path's ordering of cells (fscl_amd/csrc/device/cell_order.h: identical cells and
+    shared endpoints found by ordered comparison, the windows' galloping site search), built
+    here with g++ and checked against std::map / std::lower_bound restatements over 4 000 cell
+    lists: the host's ascending order, two ascending runs, shuffled, with duplicates, nested
+    cells and negative positions."""
+    exe = tmp_path / "cell_order_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Werror", str(ROOT / "tests" / "cpp" / "cell_order_check.cpp"),
+                    "-o", str(exe)], check=True, timeout=120)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
