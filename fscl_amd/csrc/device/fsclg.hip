@@ -2029,6 +2029,12 @@ struct fsclg_ctx {
   int n_chr = 0;
   std::vector<int> h_chr_n;
   std::vector<int32_t> h_pos, h_chr_start;
+  cellorder::SiteIndex site_index;  // window_ranges' searches (built on first use after an upload)
+  bool sidx_valid = false;
+  long long site_epoch = 0;         // site uploads indexed so far (window_ranges' memo key)
+  cellorder::RangeMemo<fsclg_cell_t, int2> wr_memo;
+  std::vector<int2> wr_need;
+  std::vector<int> wr_idx;
   int lt_hi = 0;                        // logt3 branch-2 entries [256, lt_hi) staged in LDS
   std::vector<long long> h_row_cnt;     // sites per device row
   std::vector<double> h_lt3;
@@ -2280,6 +2286,7 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   c->h_chr_n.assign(chr_n, chr_n + n_chr);
   c->h_chr_start.assign(chr_start, chr_start + n_chr);
   c->h_pos.assign(pos, pos + n_snps);
+  c->sidx_valid = false;
   c->cell_cost.clear();
   {  // |d| of a walk stays within a chromosome's span (plus grid slack): branch-2 index range
     long long span = 0;
@@ -2687,30 +2694,34 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
 // nearest SNP), merged, for the chromosomes above 2*er+1 SNPs
 static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out) {
   const long long W = 2ll * er + 1;
-  std::vector<int2> need;
-  need.reserve(n_cells);
-  int hint_chr = -1, hint = 1;  // the last search's answer: cells mostly arrive in position order
-  for (int i = 0; i < n_cells; i++) {
-    const int ch = cells[i].chr;
-    if (ch < 0 || ch >= c->n_chr) continue;
+  if (!c->sidx_valid) {
+    c->site_index.build(c->h_pos.data(), c->h_chr_start.data(), c->h_chr_n.data(), c->n_chr);
+    c->sidx_valid = true;
+    c->site_epoch++;
+  }
+  std::vector<int2>& need = c->wr_need;
+  c->wr_memo.ranges(cells, n_cells, (c->site_epoch << 32) | W, need, [&](const fsclg_cell_t& x, int2& rg) {
+    const int ch = x.chr;
+    if (ch < 0 || ch >= c->n_chr) return false;
     const long long n = c->h_chr_n[ch];
-    if (n <= W) continue;
+    if (n <= W) return false;
     const int cs = c->h_chr_start[ch], ce = cs + (int)n - 1;
     const int32_t* pos = c->h_pos.data() + cs;
-    if (ch != hint_chr) { hint_chr = ch; hint = 1; }
-    auto jof = [&](int x) { return hint = cellorder::lower_bound_from(pos, (int)n, hint, x); };
-    const int nlo = std::max(jof(cells[i].start_pos) - 1, 0), nhi = std::min(jof(cells[i].end_pos), (int)n - 1);
+    auto jof = [&](int p) { return c->site_index.find(pos, ch, (int)n, p); };
+    const int nlo = std::max(jof(x.start_pos) - 1, 0), nhi = std::min(jof(x.end_pos), (int)n - 1);
     auto wsof = [&](int nl) {
       const int near = cs + nl;
       if (near - er < cs) return cs;
       if (near + er > ce) return std::max(cs, (int)(ce - 2ll * er));
       return near - er;
     };
-    need.push_back(make_int2(wsof(nlo), wsof(nhi) + 1));
-  }
-  std::vector<int> idx(need.size());
+    rg = make_int2(wsof(nlo), wsof(nhi) + 1);
+    return true;
+  });
+  std::vector<int>& idx = c->wr_idx;
+  idx.resize(need.size());
   for (size_t k = 0; k < need.size(); k++) idx[k] = (int)k;
-  cellorder::sort_runs(idx, [&need](int a, int b) { return need[a].x < need[b].x; });
+  cellorder::sort_runs(idx, [&need](int a, int b) { return need[a].x < need[b].x; });  // in order already
   out.clear();
   for (int k : idx) {
     const int2& x = need[k];

@@ -1,7 +1,7 @@
 // CPU check of fscl_amd/csrc/device/cell_order.h (built and run by tests/test_host.py): the
 // ordered dedup of cells and endpoints against std::map restatements, over cell lists in the
 // host's order (ascending), two ascending runs, shuffled, with duplicates, nested cells and
-// negative positions; the galloping search against std::lower_bound.  Prints "ok <cases>".
+// negative positions; the bucketed site index against std::lower_bound.  Prints "ok <cases>".
 #include <stdio.h>
 
 #include <map>
@@ -59,16 +59,59 @@ int main() {
       if (a.x != ucells[u].chr || a.y != ucells[u].start_pos || b.x != ucells[u].chr || b.y != ucells[u].end_pos)
         return fail("endpoint index", it);
     }
-    // the galloping search
-    const int m = 1 + (int)(g() % 300);
-    std::vector<int32_t> pos(m);
-    int v = (int)(g() % 5) - 2;
-    for (auto& p : pos) { v += (int)(g() % 4); p = v; }
-    for (int q = 0; q < 30; q++) {
-      const int h = 1 + (int)(g() % m), x = (int)(g() % (v + 12)) - 4;
-      const int got = cellorder::lower_bound_from(pos.data(), m, std::min(h, m), x);
-      const int ref = (int)(std::lower_bound(pos.begin() + std::min(1, m), pos.end(), x) - pos.begin());
-      if (got != std::max(ref, 1)) return fail("lower_bound_from", it);
+    // the range memo over a run of calls (cells dropping out, new ones, another key): the
+    // computed range of every distinct cell, in cell order
+    {
+      cellorder::RangeMemo<Cell, I2> memo;
+      std::vector<Cell> cur = cells;
+      for (int call = 0; call < 6; call++) {
+        const long long mk = call < 4 ? 7 : 9;
+        auto f = [mk](const Cell& x, I2& r) {
+          if (x.chr == 3) return false;  // no range
+          r = I2{x.start_pos * 3 + (int)mk, x.end_pos - x.chr};
+          return true;
+        };
+        std::vector<I2> got;
+        memo.ranges(cur.data(), (int)cur.size(), mk, got, f);
+        std::map<std::tuple<int, int, int>, I2> w;
+        for (auto& x : cur) { I2 r; if (f(x, r)) w[key(x)] = r; }
+        if (got.size() != w.size()) return fail("memo count", it);
+        size_t q = 0;
+        for (auto& kv : w) {
+          if (got[q].x != kv.second.x || got[q].y != kv.second.y) return fail("memo range", it);
+          q++;
+        }
+        std::vector<Cell> nx;  // the next trial: most cells stay, a few new
+        for (auto& x : cur) if (g() % 5) nx.push_back(x);
+        for (int a = 0; a < 3; a++) nx.push_back(Cell{(int)(g() % 4), (int)(g() % 40) * grid, (int)(g() % 40) * grid + grid});
+        cur.swap(nx);
+      }
+    }
+    // the site index: every chromosome's lower_bound(pos + 1, pos + n, x)
+    const int nchr = 1 + (int)(g() % 4);
+    std::vector<int32_t> all;
+    std::vector<int32_t> cst(nchr);
+    std::vector<int> cn(nchr);
+    for (int ch = 0; ch < nchr; ch++) {
+      cst[ch] = (int32_t)all.size();
+      cn[ch] = (int)(g() % 300);  // some empty or one-site chromosomes
+      int v = (int)(g() % 200000) - 100000;
+      const int step = 1 << (g() % 18);  // sparse to dense against the 2^16-bp buckets
+      for (int i = 0; i < cn[ch]; i++) { v += (int)(g() % (unsigned)step) * (g() % 5 ? 1 : 0); all.push_back(v); }
+    }
+    cellorder::SiteIndex si;
+    si.build(all.data(), cst.data(), cn.data(), nchr);
+    for (int ch = 0; ch < nchr; ch++) {
+      const int32_t* pos = all.data() + cst[ch];
+      const int m = cn[ch];
+      if (m < 1) continue;
+      for (int q = 0; q < 40; q++) {
+        const long long span = (long long)pos[m - 1] - pos[0] + 4;
+        const int x = (int)(pos[0] - 2 + (long long)(g() % (unsigned)(span + 4)) - 2);
+        const int got = si.find(pos, ch, m, x);
+        const int ref = (int)(std::lower_bound(pos + 1, pos + m, x) - pos);
+        if (got != ref) return fail("site index", it);
+      }
     }
   }
   printf("ok %d\n", cases);

@@ -477,7 +477,7 @@ def test_c3_input_is_ascertained_and_its_fixture_is_not_degenerate():
 
 def test_cell_order_dedup_and_search(tmp_path):
     """The submit path's ordering of cells (fscl_amd/csrc/device/cell_order.h: identical cells and
-    shared endpoints found by ordered comparison, the windows' galloping site search), built
+    shared endpoints found by ordered comparison, the windows' bucketed site index), built
     here with g++ and checked against std::map / std::lower_bound restatements over 4 000 cell
     lists: the host's ascending order, two ascending runs, shuffled, with duplicates, nested
     cells and negative positions."""
