@@ -8,7 +8,7 @@ import numpy as np
 raw = np.fromfile(sys.argv[1], dtype=np.uint64)
 i, recs = 0, []
 while i < raw.size:
-    n = int(raw[i]); i += 1
+    n = int(raw[i]) & ((1 << 40) - 1); i += 1  # header: n | batch << 40 | split << 48
     recs.append(raw[i:i + 8 * n].reshape(n, 8).astype(np.int64)); i += 8 * n
 t0 = min(a[:, 0].min() for a in recs)
 ev = []
