@@ -1945,7 +1945,6 @@ struct Slot {
   double* d_win_null = nullptr;   // [n_snps], valid for (win_er, rows) while win_valid
   int win_er = -1;
   bool win_valid = false;         // win_null holds every window start, or (win_part) the ranges wdone
-  bool win_fresh = false;         // fsclg_slot_windows covered every cell the slot's next batches submit
   bool win_part = false;
   std::vector<int2> wdone;        // window starts [x, y) summed for the slot's rows, sorted, disjoint
   int2* p_wtasks = nullptr;       // pinned: the tasks of the slot's last partial window launch
@@ -1988,6 +1987,7 @@ struct Batch {
   unsigned long long* ivhist = nullptr;    // this launch measures the interval histogram (FSCLG_IVHIST)
   bool traced = false;
   std::vector<int> uidx, upos, order, sidx;
+  cellorder::RangeMemo<fsclg_cell_t, int2> wr_memo;  // its cells' window ranges at the last submit
   std::vector<unsigned long long> ekeys;
   std::vector<fsclg_cell_t> ucells;
   std::vector<int2> epos, ucell_ep;
@@ -2252,7 +2252,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->ustream))) return r;
   c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
   c->plan_dirty = true;
-  for (Slot& S : c->slot) { S.win_valid = false; S.ctab_valid = false; S.win_fresh = false; }
+  for (Slot& S : c->slot) { S.win_valid = false; S.ctab_valid = false; }
   return FSCLG_OK;
 }
 
@@ -2275,7 +2275,7 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
     if ((r = upload(&S.d_pr, pr.data(), pr.size(), c->ustream))) return r;
     if ((r = upload<double>(&S.d_chr_null, nullptr, (size_t)n_chr, c->ustream))) return r;
     if ((r = upload<double>(&S.d_win_null, nullptr, (size_t)n_snps, c->ustream))) return r;
-    S.win_valid = false; S.win_er = -1; S.ctab_valid = false; S.win_fresh = false;
+    S.win_valid = false; S.win_er = -1; S.ctab_valid = false;
     HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   }
   c->n_snps = n_snps;
@@ -2352,7 +2352,7 @@ int fsclg_slot_set_rows(fsclg_ctx* c, int slot, const uint32_t* row, const doubl
   int r;
   if ((r = ensure_row_staging(c, S))) return r;
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read the staging
-  S.win_valid = false; S.ctab_valid = false; S.win_fresh = false;
+  S.win_valid = false; S.ctab_valid = false;
   if (row) {
     uint32_t mx = 0;
     for (int i = 0; i < c->n_snps; i++) mx = row[i] > mx ? row[i] : mx;  // vectorised validation
@@ -2426,7 +2426,7 @@ int fsclg_slot_set_rows_packed(fsclg_ctx* c, int slot, const void* row, int row_
   int r;
   if ((r = ensure_null_staging(c, S))) return r;
   HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read h_null
-  S.win_valid = false; S.ctab_valid = false; S.win_fresh = false;
+  S.win_valid = false; S.ctab_valid = false;
   if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
   // read straight from the caller's portable pinned rows (one buffer can feed every device)
   const double* cn = chr_null ? S.h_null : nullptr;
@@ -2546,7 +2546,9 @@ static int window_time(fsclg_ctx* c, Slot& S) {
 // the null sums of every window of the chromosomes longer than 2*er+1 SNPs, for the slot's
 // rows (window_null_kernel on the upload stream, timed apart from the search; the host does
 // not wait for it: the slot's batches wait on the GPU, and its time is read later)
-static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out);
+typedef cellorder::RangeMemo<fsclg_cell_t, int2> WinMemo;
+static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out,
+                         WinMemo& memo);
 static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vector<int2>& todo);
 
 // window_chunk_kernel's parameters for windows of W sites: emin, the least binade in which a chunk
@@ -2612,12 +2614,12 @@ static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne, long long W) {
   return FSCLG_OK;
 }
 
-static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* cells, int n_cells) {
+static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* cells, int n_cells, WinMemo* memo) {
   const long long W = 2ll * er + 1;
   Slot& S = c->slot[slot];
   if (S.win_valid && S.win_er == er && S.win_part) {  // fsclg_slot_windows summed some: anything missing?
     std::vector<int2> need, todo;
-    window_ranges(c, er, cells, n_cells, need);
+    window_ranges(c, er, cells, n_cells, need, *memo);
     size_t d = 0;
     for (int2 x : need) {
       int a = x.x;
@@ -2692,7 +2694,8 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
 // [start, end] has its nearest SNP in [j(start) - 1, j(end)], search_snppos's j being the least
 // index in [1, n) with position >= pos (n if none), and the window start is monotone in the
 // nearest SNP), merged, for the chromosomes above 2*er+1 SNPs
-static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out) {
+static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_cells, std::vector<int2>& out,
+                         WinMemo& memo) {
   const long long W = 2ll * er + 1;
   if (!c->sidx_valid) {
     c->site_index.build(c->h_pos.data(), c->h_chr_start.data(), c->h_chr_n.data(), c->n_chr);
@@ -2700,7 +2703,7 @@ static int window_ranges(fsclg_ctx* c, int er, const fsclg_cell_t* cells, int n_
     c->site_epoch++;
   }
   std::vector<int2>& need = c->wr_need;
-  c->wr_memo.ranges(cells, n_cells, (c->site_epoch << 32) | W, need, [&](const fsclg_cell_t& x, int2& rg) {
+  memo.ranges(cells, n_cells, (c->site_epoch << 32) | W, need, [&](const fsclg_cell_t& x, int2& rg) {
     const int ch = x.chr;
     if (ch < 0 || ch >= c->n_chr) return false;
     const long long n = c->h_chr_n[ch];
@@ -2790,9 +2793,6 @@ static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, 
 int fsclg_slot_windows(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, int n_cells, int eval_range) {
   const double t0 = hprof_on() ? hnow() : 0.0;
   const int r = slot_windows_impl(c, slot, cells, n_cells, eval_range);
-  // the caller's promise (fsclg.h): the slot's batches until its next rows submit only these cells, so
-  // their submits need not check the windows again
-  if (r == FSCLG_OK && slot >= 0 && slot < NSLOT) c->slot[slot].win_fresh = true;
   if (hprof_on()) g_hprof[0] += hnow() - t0;
   return r;
 }
@@ -2813,13 +2813,13 @@ static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, 
   if (!all) return FSCLG_OK;  // no chromosome above the window: the whole-chromosome sums serve
   std::vector<int2> need;
   const double t0 = hprof_on() ? hnow() : 0.0;
-  window_ranges(c, eval_range, cells, n_cells, need);
+  window_ranges(c, eval_range, cells, n_cells, need, c->wr_memo);
   if (hprof_on()) g_hprof[5] += hnow() - t0;
   long long waves = 0;
   for (const int2& x : need) waves += (x.y - x.x + WW - 1) / WW;
   if (2 * waves >= all) {  // most windows: every one, the dense kernel's way
     S.win_valid = false;
-    return ensure_windows(c, slot, eval_range, nullptr, 0);
+    return ensure_windows(c, slot, eval_range, nullptr, 0, nullptr);
   }
   S.wdone.clear();
   S.win_valid = false;
@@ -3061,9 +3061,9 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
   }
   {
     const double t0 = hprof_on() ? hnow() : 0.0;
-    const Slot& S = c->slot[slot];
-    if (!(S.win_fresh && S.win_valid && S.win_er == eval_range))
-      if ((r = ensure_windows(c, slot, eval_range, cells, n_cells))) return r;
+    // the cells' windows (a check against what fsclg_slot_windows summed: each batch remembers its
+    // cells' ranges from its previous submit, so this is a merge of two ordered lists)
+    if ((r = ensure_windows(c, slot, eval_range, cells, n_cells, &B.wr_memo))) return r;
     if (hprof_on()) g_hprof[4] += hnow() - t0;
   }
   const double t_dd = hprof_on() ? hnow() : 0.0;

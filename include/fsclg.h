@@ -123,10 +123,9 @@ uint32_t *fsclg_slot_row_buffer(fsclg_ctx *c, int slot);
 int fsclg_slot_set_rows(fsclg_ctx *c, int slot, const uint32_t *row, const double *chr_null);
 /* the window null sums (chromosomes above 2*eval_range+1 SNPs) for the cells that the slot's
    next batches will evaluate, given before the slot's first submit of a trial: only those
-   windows when they are few, every window otherwise.  The slot's batches until its next rows
-   must then submit only these cells (or some of them): their submits do not check the windows
-   again.  Without this call a batch whose cells need windows not summed yet sums them at its
-   submit. */
+   windows when they are few, every window otherwise.  A submit checks its cells against what
+   was summed and sums any window still missing (also without this call), so a batch may
+   submit other cells too, at the cost of a second window launch. */
 int fsclg_slot_windows(fsclg_ctx *c, int slot, const fsclg_cell_t *cells, int n_cells, int eval_range);
 int fsclg_search_submit(fsclg_ctx *c, int batch, int slot, const fsclg_cell_t *cells, int n_cells, int eval_range,
                         int bp_resl);
