@@ -3022,6 +3022,8 @@ static int ensure_pinned(T** h, int* cap, int n) {
 }
 }
 
+// the key of a cell's remembered cost (cell_cost), used only to order a launch longest first:
+// distinct below 2^29 bp and 64 chromosomes, and a collision past that misorders, never miscomputes
 static unsigned long long cell_key(const fsclg_cell_t& x) {
   return ((unsigned long long)(uint32_t)x.chr << 58) ^ ((unsigned long long)(uint32_t)x.start_pos << 29) ^
          (unsigned long long)(uint32_t)x.end_pos;
