@@ -20,7 +20,7 @@ mkdir -p $OUT
 REC=/tmp/fscl_sim_ranks_$TAG.bin
 U=$(python3 -c "import sys; sys.path.insert(0, '$R'); import bench; print(bench.cpu_info()['usable_cpus'])")
 echo "usable CPUs: $U, W=$W"
-timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > /dev/null 2>&1  # warm caches
+timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/warm.log 2>&1  # warm caches (to a file: a long silent step looks hung to gpurun)
 FSCL_AMD_SIM=record:$REC timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w1_record.json 2> $OUT/w1_record.err || exit 1
 burn() {  # $1 spinning processes (BURN=yield: spinning with sched_yield, as the ranks' exchange waits do
           # after 4096 spins), each time-limited; their pids in BURN_PIDS
