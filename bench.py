@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU baseline threads (default: every CPU this process may run on)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="CPU baseline: cells in the sample")
+    ap.add_argument("--cpu-full-job", action="store_true",
+                    help="CPU baseline: also run the WHOLE job through oracle/_ref/ref_harness (the reference's "
+                         "compiled hot path under the restated scan loop) and report it beside the sample's "
+                         "extrapolation (the anchor of the extrapolation model; minutes at C2)")
     ap.add_argument("--exchange", choices=("shm", "torch"), default="shm",
                     help="multi-process exchange: the library's shared-memory all-gather, or a torch.distributed "
                          "all-reduce callback")
@@ -529,6 +533,43 @@ def _harness(snp, cfg, threads, n_cells):
     return {k: float(v) for k, v in kv.items()}
 
 
+def _harness_full(snp, cfg, threads, n_permute, wd):
+    """The whole job through the reference's compiled hot path: ref_harness scan (initial scan, then every
+    permutation trial: the active points on `threads` threads, the block permutation serial between trials,
+    as scan-chromosome.c:412-546 does), wall-clocked."""
+    harness = ROOT / "oracle" / "_ref" / "ref_harness"
+    opts = [f"--n-threads={threads}", f"--n-permute={n_permute}"]
+    if cfg.get("asc_depth", 0):
+        opts += [f"--asc-depth={cfg['asc_depth']}", f"--asc-minimum-freq={cfg.get('asc_min_freq', 1)}"]
+    t0 = time.perf_counter()
+    r = subprocess.run([str(harness), "scan", str(snp), str(Path(wd) / "cpu_full.out"), str(Path(wd) / "cpu_full.dump"),
+                        *opts], capture_output=True, text=True)
+    wall = time.perf_counter() - t0
+    kv = dict(w.split("=", 1) for w in r.stderr.split() if "=" in w)
+    if r.returncode not in (0, 3) or "scan_s" not in kv:  # 3: the job hit the reference's negative-j read (Q9)
+        raise RuntimeError(f"ref_harness scan failed ({r.returncode}): {r.stderr[-400:]}")
+    return {"job_s": wall, "scan_s": float(kv["scan_s"]), "threads": threads, "negj": int(kv.get("negj", 0)),
+            "setup_note": "job_s includes the harness's setup (input, background, tables: about a second at C2)"}
+
+
+def cpu_anchor() -> dict | None:
+    """The extrapolation model's measured anchor: the newest committed bench line with a `full_job`
+    (profiles/r*_cpu_anchor_*.json, a `--cpu-full-job` run on the GPU box)."""
+    cands = sorted((ROOT / "profiles").glob("r*_cpu_anchor_*.json"))
+    for q in reversed(cands):
+        try:
+            d = json.loads(q.read_text().strip().splitlines()[-1])
+            fj = d["cpu_baseline"]["full_job"]
+        except (OSError, ValueError, KeyError, TypeError, IndexError):
+            continue
+        return {"source": str(q.relative_to(ROOT)), "workload": d["config"]["workload"],
+                "threads": fj["threads"], "measured_job_s": fj["job_s"], "extrapolated_job_s": fj["extrapolated_job_s"],
+                "measured_over_extrapolated": fj["measured_over_extrapolated"],
+                "note": "the same box's whole job through the reference's compiled hot path, against the sample "
+                        "extrapolation this line uses: the model's error at that workload"}
+    return None
+
+
 def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, trials, units, gpu_job_s,
                  live_parity=True):
     """Returns (cpu_baseline dict, max |dCLR|, position mismatches); live_parity=False: the parity block
@@ -574,6 +615,16 @@ def cpu_baseline(args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, perm_units, 
                           "note": "one-thread per-cell time / the node's physical cores (perfect scaling, "
                                   "an upper bound for the CPU) + the serial permutations"},
           **info, "gpu_over_cpu": job_s / gpu_job_s, "gpu_over_node_linear": node_s / gpu_job_s}
+    if args.cpu_full_job:
+        full = _harness_full(snp, cfg, threads, args.n_permute if args.n_permute is not None else cfg["n_permute"], wd)
+        bl["full_job"] = {**full, "extrapolated_job_s": job_s, "measured_over_extrapolated": full["job_s"] / job_s,
+                          "units": units, "value": units / full["job_s"],
+                          "what": "the whole job (initial scan + every permutation trial with its pruning) through "
+                                  "oracle/_ref/ref_harness scan on the same threads: the measured point the "
+                                  "sample's extrapolation is checked against"}
+    anchor = cpu_anchor()
+    if anchor:
+        bl["anchor"] = anchor
     if not live_parity:
         bl["parity"] = "see the line's parity block (committed oracle fixture)"
         return bl, None, None

@@ -27,7 +27,7 @@ OUT = PKG / "_build"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("FSCL_AMD_ARCH", "gfx950")
 
-HOST_SRC = ["util.c", "input.c", "spectrum.c", "tables.c", "scan.c", "ranks.c"]
+HOST_SRC = ["util.c", "input.c", "spectrum.c", "tables.c", "perm.c", "scan.c", "ranks.c"]
 CFLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-fopenmp", "-Wall", "-Wno-unused-result",
           "-std=gnu11"]
 # iterative-ilp machine scheduling: 0.9 % (C2) / 0.4 % (C4) less time per launch, measured A/B

@@ -20,6 +20,30 @@ typedef struct { int32_t r[31]; int f, b; } fh_rand_t;
 void fh_srand(fh_rand_t *g, unsigned seed);
 int fh_rand(fh_rand_t *g);
 
+/* the block permutation as a device plan (perm.c; scan-chromosome.c:336-389) */
+typedef struct {
+  int n, n_chr;
+  const int32_t *chr_start, *chr_n, *pos;
+  const int32_t *ext;  /* fh_ext_table */
+} fh_perm_geom_t;
+typedef struct {     /* per-thread scratch of fh_plan_build */
+  fsclg_swap_t *blk;
+  int bcap;
+  uint16_t *gran;
+  int gcap;
+  int *lvl;
+  int lcap;
+} fh_plan_t;
+void fh_ext_table(int32_t *ext, const int32_t *pos, const int32_t *chr_start, const int32_t *chr_n, int n_chr,
+                  double width_mb);
+int fh_block_draw(const fh_perm_geom_t *G, double nbp, double width_mb, fh_rand_t *g, int i, int *jo,
+                  unsigned long long *negj);
+int fh_plan_build(fh_plan_t *P, const fh_perm_geom_t *G, double nbp, double width_mb, fh_rand_t *g,
+                  unsigned long long *negj, fsclg_swap_t *ent, int ecap, int32_t *grp, int gcap, int *n_ent,
+                  int *n_grp, const volatile unsigned *gen, unsigned my_gen);
+void fh_plan_free(fh_plan_t *P);
+void fh_plan_apply_u32(uint32_t *rows, int n, const fsclg_swap_t *ent, const int32_t *grp, int n_grp);
+
 /* log_fact table shared by lchoose (sm-spline.c:18-39) */
 double fh_log_fact(int n);
 void fh_log_fact_reserve(int n);

@@ -16,6 +16,8 @@
  *   fsclg_set_rows       -> the permuted snp array of one trial,
  *                           scan-chromosome.c:443 (snp_block_permute output)
  *   fsclg_slot_set_rows  -> the same for one of FSCLG_N_SLOTS trials in flight
+ *   fsclg_slot_set_rows_plan -> snp_block_permute itself (scan-chromosome.c:336-389)
+ *                           applied on the device from the host's block plan
  *   fsclg_search_submit/ -> the per-trial search_maxpos calls of
  *   fsclg_search_wait       scan_permute_thread (scan-chromosome.c:478-487),
  *                           split so that consecutive trials overlap on the GPU
@@ -151,6 +153,23 @@ int fsclg_slot_set_rows_host(fsclg_ctx *c, int slot, const uint32_t *row, const 
 /* the same with rows of row_bytes = 1, 2 or 4 bytes each (1: n_rows <= 256, 2: n_rows <= 65536):
    a narrower staging is fewer PCIe bytes for every device's upload of every trial */
 int fsclg_slot_set_rows_packed(fsclg_ctx *c, int slot, const void *row, int row_bytes, const double *chr_null);
+
+/* A trial's block permutation as a plan, applied on the device (scan-chromosome.c:336-389:
+   snp_block_permute's swaps, from the rand() stream, on the uploaded rows).  The host draws the
+   blocks and groups them (fh_plan_build, fscl_amd/csrc/host/perm.c); the device copies the
+   uploaded rows into the slot and applies the groups in order.  Within a group the entries touch
+   disjoint sites, so they run in any order.  kind 0: rows[i + t] <-> rows[j + t] for t < len, the
+   two ranges disjoint (a block, or a piece of one).  kind 1: a block whose ranges overlap,
+   |i - j| < len, the reference's sequential element swaps (a rotation of [min(i,j), min(i,j) +
+   len + |i - j|)), alone in its group.  ent and grp (n_grp + 1 offsets into ent) are host
+   memory the devices read directly (fsclg_host_alloc or fsclg_host_register) and must stay
+   unchanged until fsclg_slot_wait(c, slot) returns; only the chr_null values are copied.
+   Every range is checked against n_snps. */
+typedef struct {
+  int32_t i, j, len, kind;
+} fsclg_swap_t;
+int fsclg_slot_set_rows_plan(fsclg_ctx *c, int slot, const fsclg_swap_t *ent, const int32_t *grp, int n_grp,
+                             const double *chr_null);
 
 /* sequential window null sums (init_scan_result's sum from 0.0) for each chromosome's
    whole-chromosome window, for the rows currently set */

@@ -486,3 +486,66 @@ def test_cell_order_dedup_and_search(tmp_path):
                     "-o", str(exe)], check=True, timeout=120)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+
+
+ORC_SNP = np.dtype([("chr", "<i4"), ("pos", "<i4"), ("null_logl", "<f8"), ("obs_freq", "<i4"), ("depth_p", "<i4"),
+                    ("folded", "<i4"), ("pad", "<i4")])
+ORC_STATS = C.c_longlong * 6  # orc_stats_t: ..., negj last
+
+
+def _plan_geometry(n_chr, per_chr, chr_len, seed):
+    rng = np.random.default_rng(seed)
+    pos = np.concatenate([np.sort(rng.choice(chr_len, per_chr, replace=False)).astype(np.int32) + 1
+                          for _ in range(n_chr)])
+    chr_start = (np.arange(n_chr) * per_chr).astype(np.int32)
+    return pos, chr_start, np.full(n_chr, per_chr, np.int32)
+
+
+@pytest.mark.parametrize("geom", [
+    # (chromosomes, SNPs each, bp, trials, nbp, width Mb): C5's chromosome over 1 000 trials; the whole C5
+    # genome; short chromosomes where blocks run past the end (Q9) and overlap themselves
+    (1, 227_273, 227_000_000, 1000, 0.1, 1.0),
+    (22, 227_273, 227_000_000, 4, 0.1, 1.0),
+    (3, 2_000, 2_000_000, 400, 0.1, 1.0),
+    (2, 500, 100_000, 400, 0.01, 0.05),
+])
+def test_block_plan_is_the_sequential_block_permutation(built, geom):
+    """perm.c's plan (blocks drawn from the rand() stream, leveled, grouped; applied as the device
+    applies it, fh_plan_apply_u32) against the oracle's orc_block_permute (scan-chromosome.c:336-389,
+    Q9 repaired the same way): the same rows, the same rand() state after, the same negative-j count,
+    trial after trial of one stream"""
+    n_chr, per, L, trials, nbp, width = geom
+    pos, cs, cn = _plan_geometry(n_chr, per, L, seed=n_chr * 7 + per)
+    n = len(pos)
+    lib = fscl_amd.get_lib()
+    lib.fscl_amd_plan_permute_test.restype = C.c_int
+    lib.fscl_amd_plan_permute_test.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_double,
+                                               C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.fh_srand.argtypes = [C.c_void_p, C.c_uint]
+    orc = C.CDLL(str(ROOT / "oracle" / "_build" / "liboracle.so"))
+    orc.orc_block_permute.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p,
+                                      C.c_void_p]
+    orc.orc_srand.argtypes = [C.c_void_p, C.c_uint]
+    snps = np.zeros(n, ORC_SNP)
+    snps["chr"] = np.repeat(np.arange(n_chr), per)
+    snps["pos"] = pos
+    snps["obs_freq"] = np.arange(n)
+    p = np.zeros_like(snps)
+    g_prod, g_orc = (C.c_int32 * 33)(), (C.c_int32 * 33)()
+    lib.fh_srand(g_prod, 0xFD821A6)
+    orc.orc_srand(g_orc, 0xFD821A6)
+    st = ORC_STATS()
+    out = (C.c_longlong * 4)()
+    negj = rot = 0
+    for t in range(trials):
+        rows = np.arange(n, dtype=np.uint32)
+        assert lib.fscl_amd_plan_permute_test(n, pos.ctypes.data, cs.ctypes.data, cn.ctypes.data, n_chr, nbp, width,
+                                              g_prod, rows.ctypes.data, out) == 0
+        orc.orc_block_permute(p.ctypes.data, snps.ctypes.data, n, nbp, width, g_orc, st)
+        assert np.array_equal(rows, p["obs_freq"].astype(np.uint32)), f"trial {t}: rows differ"
+        assert list(g_prod) == list(g_orc), f"trial {t}: rand() state differs"
+        negj += out[0]
+        rot += out[3]
+        assert negj == st[5]
+    if n < 10_000:  # the edge cases this geometry is there for
+        assert negj > 0 and rot > 0, (negj, rot)

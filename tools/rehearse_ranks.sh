@@ -20,7 +20,9 @@ mkdir -p $OUT
 REC=/tmp/fscl_sim_ranks_$TAG.bin
 U=$(python3 -c "import sys; sys.path.insert(0, '$R'); import bench; print(bench.cpu_info()['usable_cpus'])")
 echo "usable CPUs: $U, W=$W"
-timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/warm.log 2>&1  # warm caches (to a file: a long silent step looks hung to gpurun)
+if [ "${WARM:-1}" = 1 ]; then  # warm caches (to a file: a long silent step looks hung to gpurun); WARM=0 skips it (C5)
+  timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/warm.log 2>&1
+fi
 FSCL_AMD_SIM=record:$REC timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w1_record.json 2> $OUT/w1_record.err || exit 1
 burn() {  # $1 spinning processes (BURN=yield: spinning with sched_yield, as the ranks' exchange waits do
           # after 4096 spins), each time-limited; their pids in BURN_PIDS
@@ -44,7 +46,18 @@ run() {  # <name> <burners> <round> [env ...]: the replay sizes its threads as t
 }
 PER=$((U / W)); [ $PER -lt 1 ] && PER=1
 for r in $(seq ${ROUNDS:-2}); do
-  for v in ${VARIANTS:-single replicated leader leader_norefine}; do
+  for v0 in ${VARIANTS:-single replicated leader leader_norefine}; do
+    # <variant>@VAR=x,VAR2=y: the variant with extra environment (e.g. leader@FSCLG_SPLIT_BUDGET=512)
+    v=${v0%%@*}; X=""; [ "$v" != "$v0" ] && X=${v0#*@}; X=${X//,/ }
+    if [ -n "$X" ]; then
+      N=$(echo "${v}_$X" | tr ' =' '_-')
+      case $v in
+        single) run $N 0 $r LOCAL_WORLD_SIZE=1 FSCL_AMD_PERM_LEADER=0 $X ;;
+        leader) run $N $((W - 1)) $r $X ;;
+        *) echo "no extra environment for $v"; exit 1 ;;
+      esac
+      continue
+    fi
     case $v in
       # one process driving W GPUs: every spare CPU speculates for it, no other ranks
       single) run single 0 $r LOCAL_WORLD_SIZE=1 FSCL_AMD_PERM_LEADER=0 ;;
