@@ -332,6 +332,81 @@ def main() -> int:
         elapsed = float(t.item())
     st = fscl_amd.get_stats()
 
+    out = bench_line(args, cfg, st, units, elapsed, n_gpus, world, n_local, n_permute, gp, setup_s)
+
+    # ---- parity of every timed job, whole job: initial scan + all permutation trials, their
+    # hits, prune draws and saved null CLRs, against the oracle's digest of the same job
+    if fx is not None:
+        digs = [points_digest(p) for p in timed_pts]
+        ok = [d == fx["dump_sha256"] for d, _ in digs]
+        bad_rows = 0
+        if not all(ok):  # locate: the fixture's sampled rows
+            k = fx["sample_every"]
+            rows = next(r for (d, r), o in zip(digs, ok) if not o)
+            bad_rows = sum(rows[i * k] != want for i, want in enumerate(fx["sample"]))
+        out["parity"] = {"scope": "full job", "fixture": f"tests/golden/fullsize.json[{fx_name}]",
+                         "what": "SHA-256 of every field of every final scan point (CLR, lalpha, sm_logl, null_logl "
+                                 "as hex; positions, windows; permute_p, permute_n, permute_finished) of each timed "
+                                 "job against the oracle's run of the same job (oracle/oracle.c, pinned by the "
+                                 "reference's own compiled code)",
+                         "jobs_checked": len(ok), "jobs_identical": sum(ok), "points": fx["n_points"],
+                         "sum_permute_n": fx["sum_permute_n"], "sampled_rows_differing": bad_rows,
+                         "negj_per_job": st["negj"] / args.steps}
+        out["max_abs_dclr"] = 0.0 if all(ok) else None
+        if not all(ok):
+            print(f"bench.py: PARITY FAILURE: {len(ok) - sum(ok)} of {len(ok)} timed jobs differ from {fx_name}",
+                  file=sys.stderr)
+    elif sfx is not None:
+        fscl_amd.srand()
+        fscl_amd.scan_chromosome(scan, tab)
+        dig, rows = points_digest(fscl_amd.points(scan))
+        k = sfx["sample_every"]
+        ok = dig == sfx["dump_sha256"]
+        out["parity"] = {"scope": "initial scan", "fixture": f"tests/golden/fullsize.json[{sfx_name}]",
+                         "what": "SHA-256 of every field of every point of the GPU's initial scan of this genome "
+                                 "against the oracle's (no fixture of the whole permutation job exists at this size)",
+                         "points": sfx["n_points"], "identical": ok,
+                         "sampled_rows_differing": 0 if ok else sum(rows[i * k] != w for i, w in enumerate(sfx["sample"]))}
+        # not the line's max |dCLR|: the permutation trials of this job are not covered by the check
+        out["parity"]["max_abs_dclr_initial_scan"] = 0.0 if ok else None
+        out["max_abs_dclr"] = None
+        out["max_abs_dclr_note"] = "initial scan only (parity.scope): no oracle fixture of the whole job"
+    elif rank == 0:
+        out["parity"] = {"scope": "initial scan" if world == 1 and n_local == 1 and not args.no_cpu_baseline else
+                         "none in this run", "note": "no oracle fixture of this exact job (tests/golden/fullsize.json)"}
+
+    # ---- CPU baseline (rank 0, one GPU): the reference's own compiled hot path
+    # (oracle/_ref/ref_harness: sm-search.c / sm-spline.c / background / asc-bias / input
+    # compiled from its sources, under oracle.c's restated scan loop -- scan-chromosome.c
+    # needs GSL headers absent here), timed on this host's cores on a bounded sample of the
+    # same job: evenly spread scan cells, one block permutation, and those cells'
+    # permutation-trial cells; the whole job's CPU time is extrapolated from the per-cell
+    # times and the job's own counts.  Then the GPU's initial scan is checked against the
+    # reference code's on a spread sample of cells... and against the oracle on all cells.
+    # Test infrastructure: timed and compared here, never called by the product.
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
+        info = cpu_info()
+        out["cpu_baseline"], scan_dclr, out["position_mismatches"] = cpu_baseline(
+            args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, n_perm_units, st["trials"] // max(1, args.steps),
+            units / args.steps, elapsed / args.steps, live_parity=fx is None and sfx is None)
+        if fx is None and sfx is None:
+            out["max_abs_dclr"] = scan_dclr
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    fscl_amd.shutdown()
+    if out.get("parity", {}).get("scope") == "full job" and out["parity"]["jobs_identical"] != out["parity"]["jobs_checked"]:
+        return 1
+    return 0
+
+
+def bench_line(args, cfg: dict, st: dict, units: float, elapsed: float, n_gpus: int, world: int, n_local: int,
+               n_permute: int, gp: int, setup_s: float) -> dict:
+    """The JSON line (every key but parity / cpu_baseline) from the library's stats of the timed jobs
+    (fscl_amd.get_stats()) and the committed profile of the workload; tests/test_host.py drives it
+    from recorded stats on the CPU."""
     # ---- the dominant kernel (search_maxpos_kernel), from HIP events on the streams it is
     # launched on.  Consecutive trials overlap on the GPU (several batch streams), so rates
     # divide by the union of the launches' intervals (busy_ms: overlap counted once);
@@ -410,7 +485,7 @@ def main() -> int:
                     "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)"}
 
     limiter["hbm_traffic_frac_of_peak"] = roof["hbm_frac"]
-    out = {
+    return {
         "metric": METRIC,
         "value": units / elapsed,
         "unit": UNIT,
@@ -449,75 +524,9 @@ def main() -> int:
                                      "host_null_s", "host_upload_s", "search_s", "prune_s", "n_dup_cells",
                                      "n_ep_saved", "wait_s", "n_crit", "n_drain", "spec_threads", "spec_posted",
                                      "spec_hits", "spec_cands", "spec_wait_s", "spec_done", "spec_gen_s",
-                                     "spec_claimed", "n_merged")},
+                                     "spec_claimed", "n_merged", "perm_leader", "plan_mode", "plan_fallback")},
     }
 
-    # ---- parity of every timed job, whole job: initial scan + all permutation trials, their
-    # hits, prune draws and saved null CLRs, against the oracle's digest of the same job
-    if fx is not None:
-        digs = [points_digest(p) for p in timed_pts]
-        ok = [d == fx["dump_sha256"] for d, _ in digs]
-        bad_rows = 0
-        if not all(ok):  # locate: the fixture's sampled rows
-            k = fx["sample_every"]
-            rows = next(r for (d, r), o in zip(digs, ok) if not o)
-            bad_rows = sum(rows[i * k] != want for i, want in enumerate(fx["sample"]))
-        out["parity"] = {"scope": "full job", "fixture": f"tests/golden/fullsize.json[{fx_name}]",
-                         "what": "SHA-256 of every field of every final scan point (CLR, lalpha, sm_logl, null_logl "
-                                 "as hex; positions, windows; permute_p, permute_n, permute_finished) of each timed "
-                                 "job against the oracle's run of the same job (oracle/oracle.c, pinned by the "
-                                 "reference's own compiled code)",
-                         "jobs_checked": len(ok), "jobs_identical": sum(ok), "points": fx["n_points"],
-                         "sum_permute_n": fx["sum_permute_n"], "sampled_rows_differing": bad_rows,
-                         "negj_per_job": st["negj"] / args.steps}
-        out["max_abs_dclr"] = 0.0 if all(ok) else None
-        if not all(ok):
-            print(f"bench.py: PARITY FAILURE: {len(ok) - sum(ok)} of {len(ok)} timed jobs differ from {fx_name}",
-                  file=sys.stderr)
-    elif sfx is not None:
-        fscl_amd.srand()
-        fscl_amd.scan_chromosome(scan, tab)
-        dig, rows = points_digest(fscl_amd.points(scan))
-        k = sfx["sample_every"]
-        ok = dig == sfx["dump_sha256"]
-        out["parity"] = {"scope": "initial scan", "fixture": f"tests/golden/fullsize.json[{sfx_name}]",
-                         "what": "SHA-256 of every field of every point of the GPU's initial scan of this genome "
-                                 "against the oracle's (no fixture of the whole permutation job exists at this size)",
-                         "points": sfx["n_points"], "identical": ok,
-                         "sampled_rows_differing": 0 if ok else sum(rows[i * k] != w for i, w in enumerate(sfx["sample"]))}
-        # not the line's max |dCLR|: the permutation trials of this job are not covered by the check
-        out["parity"]["max_abs_dclr_initial_scan"] = 0.0 if ok else None
-        out["max_abs_dclr"] = None
-        out["max_abs_dclr_note"] = "initial scan only (parity.scope): no oracle fixture of the whole job"
-    elif rank == 0:
-        out["parity"] = {"scope": "initial scan" if world == 1 and n_local == 1 and not args.no_cpu_baseline else
-                         "none in this run", "note": "no oracle fixture of this exact job (tests/golden/fullsize.json)"}
-
-    # ---- CPU baseline (rank 0, one GPU): the reference's own compiled hot path
-    # (oracle/_ref/ref_harness: sm-search.c / sm-spline.c / background / asc-bias / input
-    # compiled from its sources, under oracle.c's restated scan loop -- scan-chromosome.c
-    # needs GSL headers absent here), timed on this host's cores on a bounded sample of the
-    # same job: evenly spread scan cells, one block permutation, and those cells'
-    # permutation-trial cells; the whole job's CPU time is extrapolated from the per-cell
-    # times and the job's own counts.  Then the GPU's initial scan is checked against the
-    # reference code's on a spread sample of cells... and against the oracle on all cells.
-    # Test infrastructure: timed and compared here, never called by the product.
-    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
-        info = cpu_info()
-        out["cpu_baseline"], scan_dclr, out["position_mismatches"] = cpu_baseline(
-            args, cfg, snp, wd, info, fscl_amd, scan, tab, gp, n_perm_units, st["trials"] // max(1, args.steps),
-            units / args.steps, elapsed / args.steps, live_parity=fx is None and sfx is None)
-        if fx is None and sfx is None:
-            out["max_abs_dclr"] = scan_dclr
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    fscl_amd.shutdown()
-    if out.get("parity", {}).get("scope") == "full job" and out["parity"]["jobs_identical"] != out["parity"]["jobs_checked"]:
-        return 1
-    return 0
 
 
 def _harness(snp, cfg, threads, n_cells):

@@ -84,7 +84,8 @@ class Stats(C.Structure):  # fscl_amd_stats_t
                 ("n_devices", C.c_int), ("spec_threads", C.c_int), ("spec_posted", C.c_ulonglong),
                 ("spec_hits", C.c_ulonglong), ("spec_cands", C.c_ulonglong), ("spec_wait_s", C.c_double),
                 ("spec_done", C.c_ulonglong), ("spec_gen_s", C.c_double),
-                ("n_split_retry", C.c_ulonglong), ("spec_claimed", C.c_ulonglong), ("n_merged", C.c_ulonglong)]
+                ("n_split_retry", C.c_ulonglong), ("spec_claimed", C.c_ulonglong), ("n_merged", C.c_ulonglong),
+                ("perm_leader", C.c_int), ("plan_mode", C.c_int), ("plan_fallback", C.c_ulonglong)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

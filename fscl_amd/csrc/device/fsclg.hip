@@ -1923,6 +1923,39 @@ __global__ void __launch_bounds__(64) scatter_rows_kernel(uint2* __restrict__ pr
     for (int c = l; c < n_chr; c += 64) chr_null[c] = chr_null_src[c];
 }
 
+// A trial's block plan (fsclg_slot_set_rows_plan, scan-chromosome.c:336-389 on the device): the
+// slot's rows start as the uploaded ones (scatter_rows_kernel, row == null), then each group of
+// the plan is applied in turn.  A group's entries touch disjoint sites: one workgroup per kind-0
+// entry (<= 4096 sites, perm.c) swaps rows[i + t] <-> rows[j + t] in the row words of the
+// interleaved (position, row) array; the reads of a thread complete before its writes, and no
+// other thread of the launch touches those sites.  The row array of one slot is only written by
+// the upload stream, in stream order.
+__global__ void __launch_bounds__(256) plan_swap_kernel(uint2* __restrict__ pr, const fsclg_swap_t* __restrict__ ent,
+                                                        int e0) {
+  const fsclg_swap_t x = ent[e0 + blockIdx.x];
+  for (int t = threadIdx.x; t < x.len; t += 256) {
+    uint32_t* a = &pr[phys((uint32_t)(x.i + t))].y;
+    uint32_t* b = &pr[phys((uint32_t)(x.j + t))].y;
+    const uint32_t va = *a, vb = *b;
+    *a = vb;
+    *b = va;
+  }
+}
+
+// kind 1, a block whose source and target overlap (d = |i - j| < len): the reference's element
+// swaps in order rotate [lo, lo + len + d), out[lo + t] = in[lo + d + t] for t < len and
+// in[lo + t % d] after; through a copy of the range (two launches: all reads before any write)
+__global__ void __launch_bounds__(256) plan_rot_save_kernel(const uint2* __restrict__ pr, uint32_t* __restrict__ tmp,
+                                                            int lo, int R) {
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < R; t += gridDim.x * 256) tmp[t] = pr[phys((uint32_t)(lo + t))].y;
+}
+
+__global__ void __launch_bounds__(256) plan_rot_kernel(uint2* __restrict__ pr, const uint32_t* __restrict__ tmp,
+                                                       int lo, int len, int d) {
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < len + d; t += gridDim.x * 256)
+    pr[phys((uint32_t)(lo + t))].y = tmp[t < len ? d + t : t % d];
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------- host shim
@@ -2017,6 +2050,8 @@ struct fsclg_ctx {
   double step = 0.0;
   // snps
   uint2* d_pr0 = nullptr;         // (biased position, device row) with the unpermuted rows
+  uint32_t* d_plan_tmp = nullptr; // fsclg_slot_set_rows_plan: the range of an overlapping block
+  int plan_tmp_cap = 0;
   std::vector<uint2> h_pr0;
   int n_snps = 0;
   int32_t* d_chr_start = nullptr;
@@ -2177,7 +2212,7 @@ int fsclg_close(fsclg_ctx* c) {
   hipDeviceSynchronize();
   void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0,
                   c->d_chr_start, c->d_chr_n, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine,
-                  c->d_stats, c->d_dfail};
+                  c->d_stats, c->d_dfail, c->d_plan_tmp};
   for (void* p : ptrs) if (p) hipFree(p);
   for (Slot& S : c->slot) {
     for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null, (void*)S.d_ctab, (void*)S.d_ctree})
@@ -2442,6 +2477,62 @@ int fsclg_slot_set_rows_packed(fsclg_ctx* c, int slot, const void* row, int row_
     hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, grid, dim3(64), 0, c->ustream, S.d_pr,
                        static_cast<const uint32_t*>(row), c->d_pr0, c->n_snps, S.d_chr_null, cn, c->n_chr);
   HIPCHK(hipGetLastError(), "launch scatter_rows_kernel");
+  HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
+  return FSCLG_OK;
+}
+
+int fsclg_slot_set_rows_plan(fsclg_ctx* c, int slot, const fsclg_swap_t* ent, const int32_t* grp, int n_grp,
+                             const double* chr_null) {
+  if (!c || !c->d_pr0) return set_err(FSCLG_E_STATE, "snps not uploaded");
+  if (slot < 0 || slot >= NSLOT) return set_err(FSCLG_E_ARG, "slot");
+  if (n_grp < 0 || (n_grp > 0 && (!ent || !grp))) return set_err(FSCLG_E_ARG, "plan");
+  Slot& S = c->slot[slot];
+  if (S.users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
+  // every range inside the sites, kind-0 ranges disjoint, kind 1 alone in its group: a bad plan is
+  // an error here, never an out-of-bounds access on the device
+  const long long n = c->n_snps;
+  int max_rot = 0;
+  if (n_grp > 0 && grp[0] != 0) return set_err(FSCLG_E_ARG, "plan groups");
+  for (int q = 0; q < n_grp; q++) {
+    if (grp[q + 1] <= grp[q]) return set_err(FSCLG_E_ARG, "plan groups");
+    for (int e = grp[q]; e < grp[q + 1]; e++) {
+      const fsclg_swap_t& x = ent[e];
+      const long long d = x.i > x.j ? (long long)x.i - x.j : (long long)x.j - x.i;
+      if (x.i < 0 || x.j < 0 || x.len < 0 || x.i + (long long)x.len > n || x.j + (long long)x.len > n)
+        return set_err(FSCLG_E_ARG, "plan entry out of range");
+      if (x.kind == 0 ? (d < x.len || x.len > 4096) : (x.kind != 1 || d >= x.len || grp[q + 1] - grp[q] != 1))
+        return set_err(FSCLG_E_ARG, "plan entry");
+      if (x.kind == 1 && x.len + d > max_rot) max_rot = (int)(x.len + d);
+    }
+  }
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  int r;
+  if ((r = ensure_null_staging(c, S))) return r;
+  if (max_rot > c->plan_tmp_cap) {
+    if (c->d_plan_tmp) HIPCHK(hipFree(c->d_plan_tmp), "hipFree");
+    c->d_plan_tmp = nullptr; c->plan_tmp_cap = 0;
+    HIPCHK(hipMalloc((void**)&c->d_plan_tmp, sizeof(uint32_t) * (size_t)max_rot), "hipMalloc plan");
+    c->plan_tmp_cap = max_rot;
+  }
+  HIPCHK(hipEventSynchronize(S.ready), "hipEventSynchronize");  // the slot's last upload has read h_null
+  S.win_valid = false; S.ctab_valid = false;
+  if (chr_null) memcpy(S.h_null, chr_null, sizeof(double) * c->n_chr);
+  // the uploaded rows (and the null sums), then the groups in order on the same stream
+  hipLaunchKernelGGL(scatter_rows_kernel<uint32_t>, dim3((c->n_snps + 255) / 256), dim3(64), 0, c->ustream, S.d_pr,
+                     nullptr, c->d_pr0, c->n_snps, S.d_chr_null, chr_null ? S.h_null : nullptr, c->n_chr);
+  for (int q = 0; q < n_grp; q++) {
+    const fsclg_swap_t& x = ent[grp[q]];
+    if (x.kind == 0) {
+      hipLaunchKernelGGL(plan_swap_kernel, dim3(grp[q + 1] - grp[q]), dim3(256), 0, c->ustream, S.d_pr, ent, grp[q]);
+    } else {
+      const int lo = x.i < x.j ? x.i : x.j, d = x.i > x.j ? x.i - x.j : x.j - x.i, R = x.len + d;
+      if (d == 0) continue;  // a block swapped with itself
+      const dim3 g((unsigned)std::min((R + 255) / 256, 1024));
+      hipLaunchKernelGGL(plan_rot_save_kernel, g, dim3(256), 0, c->ustream, S.d_pr, c->d_plan_tmp, lo, R);
+      hipLaunchKernelGGL(plan_rot_kernel, g, dim3(256), 0, c->ustream, S.d_pr, c->d_plan_tmp, lo, x.len, d);
+    }
+  }
+  HIPCHK(hipGetLastError(), "launch plan kernels");
   HIPCHK(hipEventRecord(S.ready, c->ustream), "hipEventRecord");
   return FSCLG_OK;
 }

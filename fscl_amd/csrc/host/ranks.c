@@ -24,6 +24,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
 #include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -50,7 +51,7 @@ typedef struct {
   _Atomic unsigned int attached;
   _Atomic unsigned int magic;
   unsigned int world;
-  unsigned int pad;
+  unsigned int creator;              /* rank 0's pid (a segment whose creator is gone is stale) */
   unsigned long long cap;            /* bytes per area */
   char fill[128 - 32];
   shm_slot_t slot[2][SHM_MAX_RANKS]; /* by exchange parity, as the areas */
@@ -93,6 +94,29 @@ static int wait_ge_u(_Atomic unsigned int *v, unsigned int target) {
   return 0;
 }
 
+/* A segment left by a launch that died before all its ranks attached (rank 0 unlinks the name
+   only then): its creator's pid is gone, or it was never initialised and is older than a minute.
+   Returns 1 for such a segment (the CLI's default name repeats across launches). */
+static int shm_stale(const char *name) {
+  struct stat sb;
+  int stale = 0, fd = shm_open(name, O_RDONLY, 0600);
+  if (fd < 0) return 0;
+  if (fstat(fd, &sb) == 0) {
+    if ((size_t)sb.st_size < sizeof(shm_hdr_t)) stale = time(NULL) - sb.st_ctime > 60;
+    else {
+      shm_hdr_t *h = mmap(NULL, sizeof(shm_hdr_t), PROT_READ, MAP_SHARED, fd, 0);
+      if (h != MAP_FAILED) {
+        const unsigned pid = h->creator;
+        if (pid) stale = kill((pid_t)pid, 0) != 0 && errno == ESRCH;
+        else stale = time(NULL) - sb.st_ctime > 60;
+        munmap(h, sizeof(shm_hdr_t));
+      }
+    }
+  }
+  close(fd);
+  return stale;
+}
+
 fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap) {
   fh_shm_t *m;
   const size_t bytes = sizeof(shm_hdr_t) + 2 * cap;
@@ -107,6 +131,12 @@ fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap) {
   snprintf(m->name, sizeof m->name, "%s", name);
   if (rank == 0) {
     fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0 && errno == EEXIST && shm_stale(name)) {
+      logmsg(MSG_WARN, "fscl_amd: removing the stale shm segment %s (its launch died before every rank attached)\n",
+             name);
+      shm_unlink(name);
+      fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    }
     if (fd < 0) {
       if (errno == EEXIST)
         logmsg(MSG_ERROR, "fscl_amd: shm segment %s already exists: another job of the same name is running, or "
@@ -122,10 +152,19 @@ fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap) {
       close(fd); shm_unlink(name); free(m); return NULL;
     }
   } else {
-    for (;;) {  /* rank 0 creates it */
+    for (;;) {  /* rank 0 creates it (a stale one left by a dead launch is skipped: rank 0 replaces it) */
       struct stat sb;
       fd = shm_open(name, O_RDWR, 0600);
-      if (fd >= 0 && fstat(fd, &sb) == 0 && (size_t)sb.st_size >= bytes) break;
+      if (fd >= 0 && fstat(fd, &sb) == 0 && (size_t)sb.st_size >= bytes) {
+        shm_hdr_t *h = mmap(NULL, sizeof(shm_hdr_t), PROT_READ, MAP_SHARED, fd, 0);
+        int ok = 0;
+        if (h != MAP_FAILED) {
+          const unsigned pid = atomic_load_explicit(&h->magic, memory_order_acquire) == SHM_MAGIC ? h->creator : 0;
+          ok = pid && (kill((pid_t)pid, 0) == 0 || errno != ESRCH);
+          munmap(h, sizeof(shm_hdr_t));
+        }
+        if (ok) break;
+      }
       if (fd >= 0) close(fd);
       if (fh_now() - t0 > timeout_s()) { logmsg(MSG_ERROR, "fscl_amd: shm %s never appeared", name); free(m); return NULL; }
       usleep(1000);
@@ -139,6 +178,7 @@ fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap) {
   if (rank == 0) {
     m->h->world = (unsigned)world;
     m->h->cap = cap;
+    m->h->creator = (unsigned)getpid();
     atomic_store_explicit(&m->h->magic, SHM_MAGIC, memory_order_release);
   } else if (wait_ge_u(&m->h->magic, SHM_MAGIC) != 0 || m->h->world != (unsigned)world || m->h->cap != cap) {
     logmsg(MSG_ERROR, "fscl_amd: shm %s: rank set mismatch", name);

@@ -23,14 +23,14 @@ static void ROW_CAT(chr_null_sums, ROW_SFX)(const ROW_T *row, double *out) {
 }
 
 /* scan-chromosome.c:336-389 on the row array: blocks of consecutive sites (length ~ 1 +
-   Exp(nbp), extended to at least scan_width_mb on the same chromosome) are swapped into place;
-   positions never move.  Q9: a block running past the end is shifted left (j -= k - n) instead
-   of indexing p[-m] as the reference does; such events are counted. */
-static int ROW_CAT(block_permute, ROW_SFX)(ROW_T *prow, const ROW_T *row, const snp_t *snps, int n, double nbp,
-                                           double width_mb, fh_rand_t *g, unsigned long long *negj,
-                                           const volatile unsigned *gen, unsigned my_gen) {
-  int i = 0, j, k;
-  const double width = width_mb * 1e6;
+   Exp(nbp), extended to at least scan_width_mb on the same chromosome; fh_block_draw, shared
+   with the device plan of perm.c) are swapped into place; positions never move.  Q9: a block
+   running past the end is shifted left (j -= k - n) instead of indexing p[-m] as the reference
+   does; such events are counted. */
+static int ROW_CAT(block_permute, ROW_SFX)(ROW_T *prow, const ROW_T *row, int n, double nbp, double width_mb,
+                                           fh_rand_t *g, unsigned long long *negj, const volatile unsigned *gen,
+                                           unsigned my_gen) {
+  int i = 0, j, nb = 0;
   const int piece = (1 << 20) / (int)sizeof(ROW_T);
   for (i = 0; i < n; i += piece) { /* in 1 MB pieces: a cancelled candidate stops soon */
     if (gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1;
@@ -38,49 +38,27 @@ static int ROW_CAT(block_permute, ROW_SFX)(ROW_T *prow, const ROW_T *row, const 
   }
   i = 0;
   while (i < n) {
-    const int r1 = fh_rand(g), r2 = fh_rand(g);
-    if (gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1; /* speculation cancelled */
-    j = r1 / (2147483647 + 1.0) * n;
-    if (r2 == 0) k = n; /* Q10: log(0) */
-    else k = j + (int)(-1.0 / nbp * log(r2 / (2147483647 + 1.0)));
-    /* scan-chromosome.c:355-357: extend k while on j's chromosome and within width of
-       pos[j]; positions ascend within a chromosome, so the stop is a lower bound */
-    if (k >= 0 && k < n && snps[k].chr == snps[j].chr) {
-      const int c = snps[j].chr, ce = D.chr_start[c] + D.chr_n[c];
-      const int32_t pj = D.pos[j];
-      int lo = k, hi = ce, step = 1; /* first index in [k, ce) with pos - pj >= width, else ce */
-      while (lo + step < ce && (double)(D.pos[lo + step] - pj) < width) { lo += step; step <<= 1; } /* gallop */
-      if (lo + step < ce) hi = lo + step;
-      if ((double)(D.pos[lo] - pj) < width) lo++; /* lo itself is inside (or is k, unchecked) */
-      while (lo < hi) {
-        const int m = lo + (hi - lo) / 2;
-        if ((double)(D.pos[m] - pj) < width) lo = m + 1; else hi = m;
+    const int len = fh_block_draw(&PM.G, nbp, width_mb, g, i, &j, negj);
+    if ((++nb & 255) == 0 && gen && __atomic_load_n(gen, __ATOMIC_RELAXED) != my_gen) return -1; /* cancelled */
+    /* scan-chromosome.c:365-372: swap p[i++] with p[j++] while j < k and i < n; disjoint
+       ranges in one vectorisable pass, overlapping ones element by element as written */
+    if (len > 0 && (j >= i + len || i >= j + len)) {
+      ROW_T *__restrict a = prow + i, *__restrict b = prow + j;
+      int t;
+      for (t = 0; t < len; t++) {
+        const ROW_T x = a[t];
+        a[t] = b[t];
+        b[t] = x;
       }
-      k = lo;
-    }
-    if (i + (k - j) >= n) k = n;
-    if (k > n) { (*negj)++; j -= k - n; k = n; }
-    {
-      /* scan-chromosome.c:365-372: swap p[i++] with p[j++] while j < k and i < n; disjoint
-         ranges in one vectorisable pass, overlapping ones element by element as written */
-      const int len = (k - j < n - i) ? k - j : n - i;
-      if (len > 0 && (j >= i + len || i >= j + len)) {
-        ROW_T *__restrict a = prow + i, *__restrict b = prow + j;
-        int t;
-        for (t = 0; t < len; t++) {
-          const ROW_T x = a[t];
-          a[t] = b[t];
-          b[t] = x;
-        }
-        i += len;
-        j += len;
-      }
-      for (; j < k && i < n && j < n; i++, j++) {
-        const ROW_T t = prow[i];
-        prow[i] = prow[j];
-        prow[j] = t;
+    } else {
+      int t;
+      for (t = 0; t < len; t++) {
+        const ROW_T x = prow[i + t];
+        prow[i + t] = prow[j + t];
+        prow[j + t] = x;
       }
     }
+    if (len > 0) i += len;
   }
   return 0;
 }

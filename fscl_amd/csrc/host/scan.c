@@ -491,6 +491,51 @@ static void prepare(scan_t *s, sm_ptable_t *sm) {
 static int g_null_nt = 0;
 static int null_threads(void) { return g_null_nt > 0 ? g_null_nt : omp_get_max_threads(); }
 
+/* The block permutation's geometry (perm.c: the 1 Mb extension's end of every site, for the
+   scan's sites and scan_width_mb) and the device plan mode: when no trial reads
+   a whole-chromosome null sum -- every chromosome longer than its window, C5 -- the host needs
+   no permuted rows, and each trial's permutation goes to the devices as its plan
+   (fsclg_slot_set_rows_plan): ~16 B per block instead of rb bytes per site, and the host's part
+   is drawing the blocks (~50 ns each) instead of an O(n) copy and swap pass. */
+typedef struct { int32_t n_ent, n_grp, ok, pad; } plan_hdr_t;
+static struct {
+  int32_t *ext;        /* fh_ext_table of D's sites for ext_width */
+  double ext_width;
+  int ext_n;
+  const void *ext_key;
+  fh_perm_geom_t G;
+  int on;              /* plan mode in the current permute_pipelined call */
+  int ecap, gcap;      /* a plan buffer's capacity: entries, groups */
+  size_t bytes;        /* a plan buffer's size */
+} PM;
+
+static void perm_geom(double width_mb) {
+  if (!PM.ext || PM.ext_n != D.n_snps_key || PM.ext_width != width_mb || PM.ext_key != (const void *)D.pos) {
+    free(PM.ext);
+    PM.ext = fh_malloc(sizeof(int32_t) * (size_t)(D.n_snps_key ? D.n_snps_key : 1), "extension table");
+    fh_ext_table(PM.ext, D.pos, D.chr_start, D.chr_n, D.n_chr, width_mb);
+    PM.ext_n = D.n_snps_key; PM.ext_width = width_mb; PM.ext_key = D.pos;
+  }
+  PM.G.n = D.n_snps_key; PM.G.n_chr = D.n_chr; PM.G.chr_start = D.chr_start; PM.G.chr_n = D.chr_n;
+  PM.G.pos = D.pos; PM.G.ext = PM.ext;
+}
+
+static int32_t *plan_grp(void *buf) { return (int32_t *)((char *)buf + sizeof(plan_hdr_t)); }
+static fsclg_swap_t *plan_ent(void *buf) {
+  return (fsclg_swap_t *)((char *)buf + sizeof(plan_hdr_t) + ((sizeof(int32_t) * (size_t)(PM.gcap + 1) + 15) & ~(size_t)15));
+}
+
+/* one trial's plan into a plan buffer from rand() state *g (advanced); 0, -1 cancelled, -2 it did
+   not fit (hdr->ok = 0: the trial's rows are built on the host instead) */
+static int plan_into(void *buf, fh_plan_t *P, double nbp, double width_mb, fh_rand_t *g, unsigned long long *negj,
+                     const volatile unsigned *gen, unsigned my_gen) {
+  plan_hdr_t *h = buf;
+  const int r = fh_plan_build(P, &PM.G, nbp, width_mb, g, negj, plan_ent(buf), PM.ecap, plan_grp(buf), PM.gcap,
+                              &h->n_ent, &h->n_grp, gen, my_gen);
+  h->ok = r == 0;
+  return r;
+}
+
 /* the row-array routines at each staging width (rows_impl.h), and their dispatch on D.rb */
 #define ROW_T uint8_t
 #define ROW_SFX 8
@@ -514,11 +559,11 @@ static void chr_null_sums(const void *row, double *out) {
   else chr_null_sums_32(row, out);
 }
 
-static int block_permute(void *prow, const void *row, const snp_t *snps, int n, double nbp, double width_mb,
-                         fh_rand_t *g, unsigned long long *negj, const volatile unsigned *gen, unsigned my_gen) {
-  if (D.rb == 1) return block_permute_8(prow, row, snps, n, nbp, width_mb, g, negj, gen, my_gen);
-  if (D.rb == 2) return block_permute_16(prow, row, snps, n, nbp, width_mb, g, negj, gen, my_gen);
-  return block_permute_32(prow, row, snps, n, nbp, width_mb, g, negj, gen, my_gen);
+static int block_permute(void *prow, const void *row, int n, double nbp, double width_mb, fh_rand_t *g,
+                         unsigned long long *negj, const volatile unsigned *gen, unsigned my_gen) {
+  if (D.rb == 1) return block_permute_8(prow, row, n, nbp, width_mb, g, negj, gen, my_gen);
+  if (D.rb == 2) return block_permute_16(prow, row, n, nbp, width_mb, g, negj, gen, my_gen);
+  return block_permute_32(prow, row, n, nbp, width_mb, g, negj, gen, my_gen);
 }
 
 static int chr_null_sums_1t(const void *row, double *out, const volatile unsigned *gen, unsigned my_gen) {
@@ -581,6 +626,22 @@ static void exchange_points_flags(fsclg_point_t *out, int n, int lo, int hi, uns
 }
 
 static void exchange_points(fsclg_point_t *out, int n, int lo, int hi) { exchange_points_flags(out, n, lo, hi, NULL); }
+
+/* every rank's `word` must be the same (collective; not in a rehearsal replay, whose exchanges
+   are the recorded batches) */
+static void ranks_agree(const char *what, uint64_t word) {
+  fsclg_point_t *a;
+  int r;
+  if (D.world <= 1 || D.sim) return;
+  a = fh_calloc((size_t)D.world + 1, sizeof(fsclg_point_t), "agree");
+  memcpy(&a[D.rank].lalpha, &word, sizeof word);
+  a[D.rank].flags = 1;
+  exchange_points(a, D.world, D.rank, D.rank + 1);
+  for (r = 0; r < D.world; r++)
+    if (a[r].flags != 1 || memcmp(&a[r].lalpha, &word, sizeof word) != 0)
+      logmsg(MSG_FATAL, "fscl_amd: ranks disagree on %s (rank %d vs rank %d)", what, D.rank, r);
+  free(a);
+}
 
 /* the cost of a cell: its window size (snp_likelihood terms scale with it) */
 static double window_cost(int chr, int eval_range) {
@@ -700,6 +761,14 @@ static void slot_upload_buf(int slot, const void *rows, const double *nul) {
 
 static void slot_upload(int slot, const double *nul) { slot_upload_buf(slot, D.stage[slot], nul); }
 
+/* plan mode: the trial's plan (a plan buffer) to the slot on every local device */
+static void slot_upload_plan(int slot, void *buf, const double *nul) {
+  const plan_hdr_t *h = buf;
+  int l;
+  for (l = 0; l < D.n_dev; l++)
+    dev_check(fsclg_slot_set_rows_plan(D.ctx[l], slot, plan_ent(buf), plan_grp(buf), h->n_grp, nul), "set rows (plan)");
+}
+
 static volatile sig_atomic_t g_sigint = 0;
 static struct timeval g_last_dump;
 static double g_sigint_window = 10.;  /* seconds; FSCL_AMD_SIGINT_WINDOW_MS (tests) shortens it */
@@ -782,6 +851,7 @@ static struct {
   int stop;
   fh_rand_t base;         /* the posted job: S, and the draw counts to build */
   int n_job, next, running;
+  int n_keep;             /* workers with an index >= n_keep exit (spec_start shrinking the team) */
   int d[SPEC_MAX], bi[SPEC_MAX], state[SPEC_MAX];  /* 0 queued, 1 running, 2 done, 3 cancelled */
   fh_rand_t end[SPEC_MAX];
   unsigned long long negj[SPEC_MAX];
@@ -790,15 +860,18 @@ static struct {
   double nbp, width_mb;
   pbuf_t pb[FSCLG_N_SLOTS + 3 * SPEC_MAX + 1];
   int n_pb, pb_cap, pb_nchr, pb_rb;
+  size_t pb_bytes;        /* one buffer: a trial's rows (rb bytes per site) or, in plan mode, its plan */
+  fh_plan_t plan[SPEC_MAX + 1];  /* each worker's plan scratch; [SPEC_MAX]: the main thread's */
   int pb_in_pool;         /* the buffers are the leader's pool's (not owned here) */
-} SP = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
+} SP = {.mu = PTHREAD_MUTEX_INITIALIZER, .cv = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER,
+        .n_keep = SPEC_MAX};
 
 static void *spec_worker(void *arg) {
-  (void)arg;
+  const int w = (int)(intptr_t)arg;
   pthread_mutex_lock(&SP.mu);
   for (;;) {
-    while (!SP.stop && SP.next >= SP.n_job) pthread_cond_wait(&SP.cv, &SP.mu);
-    if (SP.stop) break;
+    while (!SP.stop && w < SP.n_keep && SP.next >= SP.n_job) pthread_cond_wait(&SP.cv, &SP.mu);
+    if (SP.stop || w >= SP.n_keep) break;
     {
       const int c = SP.next++;
       const unsigned my = SP.gen;
@@ -812,8 +885,12 @@ static void *spec_worker(void *arg) {
       pthread_mutex_unlock(&SP.mu);
       const double t0 = fh_now();
       for (t = 0; t < d; t++) (void)fh_rand(&r);
-      ok = block_permute(b->buf, D.rowp, SP.snps, SP.n, SP.nbp, SP.width_mb, &r, &negj, &SP.gen, my) == 0 &&
-           chr_null_sums_1t(b->buf, b->nul, &SP.gen, my) == 0;
+      if (PM.on) { /* the plan only (no whole-chromosome null sums are read in plan mode) */
+        ok = plan_into(b->buf, SP.plan + w, SP.nbp, SP.width_mb, &r, &negj, &SP.gen, my) == 0;
+        memset(b->nul, 0, sizeof(double) * (size_t)(D.n_chr ? D.n_chr : 1));
+      } else
+        ok = block_permute(b->buf, D.rowp, SP.n, SP.nbp, SP.width_mb, &r, &negj, &SP.gen, my) == 0 &&
+             chr_null_sums_1t(b->buf, b->nul, &SP.gen, my) == 0;
       pthread_mutex_lock(&SP.mu);
       SP.running--;
       if (ok && SP.gen == my) {
@@ -887,8 +964,18 @@ static int spec_threads_wanted(void) {
 
 static void spec_start(void) {
   const int want = spec_threads_wanted();
+  if (SP.n_th > want) {  /* a layout with fewer workers than the last call's (no job is posted here) */
+    int t;
+    pthread_mutex_lock(&SP.mu);
+    SP.n_keep = want;
+    pthread_cond_broadcast(&SP.cv);
+    pthread_mutex_unlock(&SP.mu);
+    for (t = want; t < SP.n_th; t++) pthread_join(SP.th[t], NULL);
+    SP.n_th = want;
+    SP.n_keep = SPEC_MAX;
+  }
   while (SP.n_th < want) {
-    if (pthread_create(&SP.th[SP.n_th], NULL, spec_worker, NULL) != 0) break;
+    if (pthread_create(&SP.th[SP.n_th], NULL, spec_worker, (void *)(intptr_t)SP.n_th) != 0) break;
     SP.n_th++;
   }
 }
@@ -906,6 +993,7 @@ static void spec_stop(void) {
   if (!SP.pb_in_pool)
     for (t = 0; t < SP.n_pb; t++) { fsclg_host_free(SP.pb[t].buf); free(SP.pb[t].nul); }
   SP.n_pb = SP.pb_cap = SP.pb_nchr = SP.pb_rb = SP.pb_in_pool = 0;
+  SP.pb_bytes = 0;
 }
 
 /* candidates posted per trial: two per worker thread (a C4 candidate takes ~0.7 ms of one
@@ -917,21 +1005,26 @@ static int spec_ncand(void) { return SP.n_th * 2 < SPEC_MAX ? SP.n_th * 2 : SPEC
    and the main thread's own (no job posted) */
 static int pb_count(int K) { return K + spec_ncand() + SP.n_th + 1; }
 
+/* one buffer's bytes: a trial's rows, or its plan in plan mode */
+static size_t pb_item_bytes(int n_snps) { return PM.on ? PM.bytes : (size_t)D.rb * (size_t)(n_snps ? n_snps : 1); }
+
 /* buffers for K slots, the candidates and the main thread's own (no job posted) */
 static void pb_reserve(int n_snps, int K) {
   const int want = pb_count(K);
+  const size_t item = pb_item_bytes(n_snps);
   int b;
   if (SP.pb_in_pool) { SP.n_pb = 0; SP.pb_in_pool = 0; SP.pb_cap = 0; }
-  if (SP.pb_cap < n_snps || SP.pb_nchr < D.n_chr || SP.pb_rb != D.rb) {
+  if (SP.pb_cap < n_snps || SP.pb_nchr < D.n_chr || SP.pb_rb != D.rb || SP.pb_bytes != item) {
     for (b = 0; b < SP.n_pb; b++) { fsclg_host_free(SP.pb[b].buf); free(SP.pb[b].nul); }
     SP.n_pb = 0;
     SP.pb_cap = n_snps;
     SP.pb_nchr = D.n_chr;
     SP.pb_rb = D.rb;
+    SP.pb_bytes = item;
   }
   for (; SP.n_pb < want; SP.n_pb++) {
     pbuf_t *p = SP.pb + SP.n_pb;
-    p->buf = fsclg_host_alloc((size_t)D.rb * (SP.pb_cap ? SP.pb_cap : 1));
+    p->buf = fsclg_host_alloc(item);
     if (!p->buf) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
     p->nul = fh_malloc(sizeof(double) * (SP.pb_nchr ? SP.pb_nchr : 1), "null sums");
   }
@@ -963,7 +1056,7 @@ static void slot_release(int slot) {
 /* collective: a pool large enough for the leader's buffers (K slots, two per worker thread, one
    for the main thread), then (leader) the buffers carved from it */
 static void pool_setup(int n_snps, int K) {
-  const size_t rows = ((size_t)D.rb * (size_t)(n_snps ? n_snps : 1) + 4095) & ~(size_t)4095;
+  const size_t rows = (pb_item_bytes(n_snps) + 4095) & ~(size_t)4095;  /* rows, or a plan */
   const size_t nulb = ((sizeof(double) * (size_t)(D.n_chr ? D.n_chr : 1)) + 255) & ~(size_t)255;
   const int nbuf = pb_count(K);
   const size_t want = (size_t)nbuf * (rows + nulb);
@@ -1005,7 +1098,7 @@ static void pool_setup(int n_snps, int K) {
   }
   SP.n_pb = nbuf;
   SP.pb_in_pool = 1;
-  SP.pb_cap = n_snps; SP.pb_nchr = D.n_chr; SP.pb_rb = D.rb;
+  SP.pb_cap = n_snps; SP.pb_nchr = D.n_chr; SP.pb_rb = D.rb; SP.pb_bytes = pb_item_bytes(n_snps);
 }
 
 static void pool_drop(void) {
@@ -1285,10 +1378,38 @@ static int spec_candidates(const scan_t *s, const pqueue_t *pq, const trial_batc
   return nd;
 }
 
+/* plan mode for this permute_pipelined call (PM.on): only when no chromosome's whole-chromosome
+   null sum is read (the host never needs the permuted rows) and a plan is smaller than the rows;
+   the buffers are sized from one plan drawn from a copy of the stream (every rank draws the same).
+   FSCL_AMD_PLAN=0: never; FSCL_AMD_PLAN_ECAP=m (tests): buffers of m entries, so that a plan can
+   fail to fit and the trial falls back to rows built on the host */
+static int plan_mode_setup(double nbp, double width_mb, const fh_rand_t *g) {
+  const char *e = getenv("FSCL_AMD_PLAN"), *ec = getenv("FSCL_AMD_PLAN_ECAP");
+  const int n = D.n_snps_key, ecap0 = n + n / 4096 + 16, gcap0 = 1 << 16;
+  fh_rand_t r = *g;
+  unsigned long long nj = 0;
+  fsclg_swap_t *ent;
+  int32_t *grp;
+  int ne = 0, ng = 0, st;
+  if ((e && atoi(e) == 0) || !D.chr_list || D.n_chr_list > 0 || n <= 0) return 0;
+  ent = fh_malloc(sizeof(fsclg_swap_t) * (size_t)ecap0, "plan");
+  grp = fh_malloc(sizeof(int32_t) * (size_t)(gcap0 + 1), "plan");
+  st = fh_plan_build(SP.plan + SPEC_MAX, &PM.G, nbp, width_mb, &r, &nj, ent, ecap0, grp, gcap0, &ne, &ng, NULL, 0);
+  free(ent); free(grp);
+  if (st != 0) return 0;
+  PM.ecap = 2 * ne + 4096 < ecap0 ? 2 * ne + 4096 : ecap0;
+  PM.gcap = 2 * ng + 1024;
+  if (ec) PM.ecap = atoi(ec) > 0 ? atoi(ec) : 1;
+  PM.bytes = sizeof(plan_hdr_t) + ((sizeof(int32_t) * (size_t)(PM.gcap + 1) + 15) & ~(size_t)15) +
+             sizeof(fsclg_swap_t) * (size_t)PM.ecap;
+  return PM.bytes <= (size_t)D.rb * (size_t)n;
+}
+
 static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eval_range, int bp_resl,
                               int large_grid_sp, double scan_width_mb, fh_rand_t *g, int save) {
   const char *env = getenv("FSCL_AMD_DEPTH");
   const int K = env ? (atoi(env) < 2 ? 2 : (atoi(env) > FSCLG_N_SLOTS ? FSCLG_N_SLOTS : atoi(env))) : 4;
+  const int no_merge = getenv("FSCL_AMD_NO_MERGE") != NULL;  /* read once: every rank must decide alike */
   int *act, n_act = s->n_scan_pts, i, k, trial = -1, done = -1;
   pqueue_t *pq;
   double *nul[FSCLG_N_SLOTS];
@@ -1317,16 +1438,25 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     g_null_nt = usable_cpus() - local + 1;
     if (g_null_nt < 1) g_null_nt = 1;
   }
+  PM.on = plan_mode_setup(permute_nbp, scan_width_mb, g);
+  D.st.plan_mode = PM.on;
+  /* the switches every rank's batches and collectives follow must agree (an environment variable
+     set on one rank only would otherwise diverge the exchanges) */
+  ranks_agree("FSCL_AMD_DEPTH / FSCL_AMD_NO_MERGE / FSCL_AMD_PERM_LEADER / FSCL_AMD_PLAN*",
+              (uint64_t)K | (uint64_t)no_merge << 8 | (uint64_t)PL.on << 9 | (uint64_t)PM.on << 10 |
+              (uint64_t)(PM.on ? PM.ecap : 0) << 11 | (uint64_t)(PM.on ? PM.gcap : 0) << 40);
   spec_start();
   D.st.spec_threads = SP.n_th;
   if (PL.on) pool_setup(s->n_snps, K);
   else pb_reserve(s->n_snps, K);
+  D.st.perm_leader = PL.on;
   SP.snps = s->snps; SP.n = s->n_snps; SP.nbp = permute_nbp; SP.width_mb = scan_width_mb;
   for (;;) {
     const int slot = (trial + 1) % K;
     trial_batch_t *B = &Bt[slot];
     double tp = fh_now();
     void *prow;
+    int rows_here = 0;  /* plan mode: this trial's rows were built on the host into D.stage[slot] */
     tr[0] = tp;
     /* the slot's previous trial: its bulk results (no draws among them) */
     if (B->submitted) {
@@ -1342,11 +1472,18 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
          after it (the prune draws that follow are this rank's own, the same as the leader's) */
       size_t ro, no;
       unsigned long long nj;
+      fh_rand_t g0 = *g;
       if (fh_pool_take(PL.pool, &ro, &no, g, &nj) != 0) logmsg(MSG_FATAL, "fscl_amd: permutation pool: no leader");
-      D.st.negj += nj;
       prow = fh_pool_data(PL.pool) + ro;
       pnul = (double *)(fh_pool_data(PL.pool) + no);
       from_spec = 1;  /* the null sums come with it */
+      if (PM.on && !((plan_hdr_t *)prow)->ok) {  /* a plan that did not fit: the rows, from this rank's own stream */
+        unsigned long long nj2 = 0;
+        block_permute(D.stage[slot], D.rowp, s->n_snps, permute_nbp, scan_width_mb, &g0, &nj2, NULL, 0);
+        if (memcmp(&g0, g, sizeof g0) != 0 || nj2 != nj) logmsg(MSG_FATAL, "fscl_amd: permutation pool: stream mismatch");
+        rows_here = 1;
+      }
+      D.st.negj += nj;
     } else {
       const unsigned long long negj0 = D.st.negj;
       /* this trial's permutation: the candidate for the previous trial's draw count, else built here */
@@ -1354,13 +1491,28 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       from_spec = bi >= 0;
       if (bi < 0) {
         bi = pb_get();
-        block_permute(SP.pb[bi].buf, D.rowp, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
+        if (PM.on) {
+          const fh_rand_t g0 = *g;
+          unsigned long long nj = 0;
+          if (plan_into(SP.pb[bi].buf, SP.plan + SPEC_MAX, permute_nbp, scan_width_mb, g, &nj, NULL, 0) == 0)
+            D.st.negj += nj;
+          else {  /* the plan did not fit its buffer: this trial's rows on the host (hdr.ok = 0 tells the ranks) */
+            *g = g0;
+            block_permute(D.stage[slot], D.rowp, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
+            rows_here = 1;
+            D.st.plan_fallback++;
+          }
+        } else
+          block_permute(SP.pb[bi].buf, D.rowp, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
       }
       SP.pb[bi].owner = slot;
       prow = SP.pb[bi].buf;
       pnul = SP.pb[bi].nul;
       if (PL.on) {  /* the leader: complete and publish it */
-        if (!from_spec) chr_null_sums(prow, pnul);
+        if (!from_spec) {
+          if (PM.on) memset(pnul, 0, sizeof(double) * (D.n_chr ? D.n_chr : 1));
+          else chr_null_sums(prow, pnul);
+        }
         from_spec = 1;
         if (fh_pool_publish(PL.pool, (size_t)((char *)prow - fh_pool_data(PL.pool)),
                             (size_t)((char *)pnul - fh_pool_data(PL.pool)), g, D.st.negj - negj0) != 0)
@@ -1376,15 +1528,20 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     if (n_act == 0 || trial > n_perm) break;
     tp = fh_now();
     tr[2] = tp;
-    if (!from_spec) chr_null_sums(prow, pnul);  /* a candidate carries its own */
+    if (!from_spec && !PM.on) chr_null_sums(prow, pnul);  /* a candidate carries its own; plan mode reads none */
+    if (!from_spec && PM.on) memset(pnul, 0, sizeof(double) * (D.n_chr ? D.n_chr : 1));
     D.st.host_null_s += fh_now() - tp;
     memcpy(nul[slot], pnul, sizeof(double) * (D.n_chr ? D.n_chr : 1));
     tp = fh_now();
-    if (PL.on && !PL.registered) {  /* the pool is not page-locked here: through the slot's own staging */
-      memcpy(D.stage[slot], prow, (size_t)D.rb * (size_t)s->n_snps);
-      prow = D.stage[slot];
+    if (rows_here) slot_upload_buf(slot, D.stage[slot], nul[slot]);
+    else {
+      if (PL.on && !PL.registered) {  /* the pool is not page-locked here: through the slot's own staging */
+        memcpy(D.stage[slot], prow, PM.on ? PM.bytes : (size_t)D.rb * (size_t)s->n_snps);
+        prow = D.stage[slot];
+      }
+      if (PM.on) slot_upload_plan(slot, prow, nul[slot]);
+      else slot_upload_buf(slot, prow, nul[slot]);
     }
-    slot_upload_buf(slot, prow, nul[slot]);
     D.st.host_upload_s += fh_now() - tp;
     tp = fh_now();
     A.n = B->n = 0;
@@ -1411,7 +1568,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
        later.  Merged in ascending point order (the blocking batch's draws go in that order; the
        merged points cannot draw).  The decision depends only on the counts: the same on every
        rank.  FSCL_AMD_NO_MERGE=1: never. */
-    if (B->n > 0 && A.n + B->n <= 32 * D.world * D.n_dev && !getenv("FSCL_AMD_NO_MERGE") &&
+    if (B->n > 0 && A.n + B->n <= 32 * D.world * D.n_dev && !no_merge &&
         merged_max_share(s, &A, B, eval_range) <= 32) {
       int ia = A.n - 1, ib = B->n - 1, o = A.n + B->n - 1;
       while (ib >= 0) {  /* merge from the back, in place in A (its capacity holds every active point) */
@@ -1509,6 +1666,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   spec_quiesce();
   PL.on = 0;
   PL.sizing = 0;
+  PM.on = 0;
   g_null_nt = 0;
   if (tt) fclose(tt);
   tb_free(&A);
@@ -1588,7 +1746,7 @@ static void tb_build(long j) {
   if (t <= TB.n_perm) {
     fh_rand_t g;
     fh_srand(&g, tp_trial_seed(g_pseed, t));
-    block_permute(TB.buf[b], D.rowp, TB.snps, TB.n, TB.nbp, TB.width_mb, &g, &negj, NULL, 0);
+    block_permute(TB.buf[b], D.rowp, TB.n, TB.nbp, TB.width_mb, &g, &negj, NULL, 0);
     chr_null_sums_1t(TB.buf[b], TB.nul[b], &zero, 0);
   }
   pthread_mutex_lock(&TB.mu);
@@ -1822,6 +1980,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   D.n_chr_list = 0;
   for (i = 0; i < D.n_chr; i++)
     if ((long long)D.chr_n[i] <= 2ll * eval_range + 1) D.chr_list[D.n_chr_list++] = i;
+  perm_geom(scan_width_mb);
   if (g_pmode == FSCL_AMD_PERMUTE_THROUGHPUT) { /* the rand() stream is not used */
     permute_throughput(s, n_perm, permute_nbp, eval_range, bp_resl, large_grid_sp, scan_width_mb, save);
     goto done;
@@ -1840,7 +1999,7 @@ void scan_permute(scan_t *s, sm_ptable_t *sm, int n_perm, double permute_nbp, do
   for (;;) {
     double tp = fh_now();
     prow = slot_stage(0);
-    block_permute(prow, D.rowp, s->snps, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
+    block_permute(prow, D.rowp, s->n_snps, permute_nbp, scan_width_mb, g, &D.st.negj, NULL, 0);
     D.st.host_perm_s += fh_now() - tp;
     trial++;
     for (i = k = 0; i < n_act; i++)

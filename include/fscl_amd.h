@@ -232,6 +232,12 @@ typedef struct {
   unsigned long long n_split_retry; /* fsclg_stats_t: split launches re-run unsplit */
   unsigned long long spec_claimed;  /* chosen candidates not started yet, built by the main thread instead */
   unsigned long long n_merged;      /* scan_permute: bulk cells evaluated in their trial's blocking batch */
+  int perm_leader;        /* scan_permute: 1 if the node leader's shared permutation pool ran (one process
+                             per GPU), 0 if this rank built its own permutations (single process, or the
+                             pool's fallback when the shared segment could not be made) */
+  int plan_mode;          /* scan_permute: 1 if the trials' permutations went to the devices as plans
+                             (fsclg_slot_set_rows_plan), 0 as rows */
+  unsigned long long plan_fallback; /* plan mode: trials whose plan did not fit its buffer (rows instead) */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

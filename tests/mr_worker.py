@@ -35,7 +35,8 @@ def main() -> int:
     fscl_amd.run(snp, out, **_kw(opts))
     st = fscl_amd.get_stats()
     dist.barrier()
-    print(f"rank {rank}: gp_evals {st['gp_evals']} spec_threads {st['spec_threads']} negj {st['negj']}",
+    print(f"rank {rank}: gp_evals {st['gp_evals']} spec_threads {st['spec_threads']} negj {st['negj']} "
+          f"perm_leader {st['perm_leader']} plan_mode {st['plan_mode']} plan_fallback {st['plan_fallback']}",
           file=sys.stderr)
     dist.destroy_process_group()
     return 0

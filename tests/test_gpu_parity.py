@@ -39,6 +39,8 @@ def _kw(options):
             kw["large_grid_sp"] = int(v)
         elif k == "permute-nbp":
             kw["permute_nbp"] = float(v)
+        elif k == "eval-range":
+            kw["eval_range"] = int(v)
         elif k == "sweep-width":
             kw["scan_width_mb"] = float(v)
         else:
@@ -314,6 +316,67 @@ def test_two_ranks_on_one_gpu_match_one_rank(built, tmp, exchange):
         assert "spec_threads 0" in errs[1], errs[1][-400:]
         # and both ranks' devices read the shared pool directly (page-locked, no copy)
         assert not any("could not be page-locked" in e or "permutation pool" in e for e in errs), errs
+
+
+def _windowed_genome(tmp, seed=93):
+    """two 8 000-SNP chromosomes: with --eval-range=300 every window is a proper one (no chromosome's
+    whole null sum is read), so the trials run in plan mode"""
+    snp = tmp / "plan.snp"
+    synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=8_000_000, snps_per_chr=8000, n=60, seed=seed,
+                                                  sweeps_per_chr=2))
+    return snp, ["--coarse-grid-spacing=100000", "--n-permute=60", "--eval-range=300"]
+
+
+@pytest.mark.parametrize("variant", ["plan", "rows", "fallback"])
+def test_block_plan_on_the_device_matches_oracle(built, tmp, monkeypatch, variant):
+    """Each trial's block permutation as a plan the device applies (fsclg_slot_set_rows_plan,
+    DESIGN.md §5.6): the default where no whole-chromosome null sum is read; FSCL_AMD_PLAN=0 the
+    rows built on the host; FSCL_AMD_PLAN_ECAP=1 plan buffers too small for any plan, so every
+    trial falls back to host rows.  60 permutations with pruning: bit-identical to the oracle."""
+    snp, opts = _windowed_genome(tmp)
+    if variant == "rows":
+        monkeypatch.setenv("FSCL_AMD_PLAN", "0")
+    if variant == "fallback":
+        monkeypatch.setenv("FSCL_AMD_PLAN_ECAP", "1")
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
+    fscl_amd.reset_stats()
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
+    st = fscl_amd.get_stats()
+    pts = fscl_amd.points(scan)
+    assert (pts["permute_n"] < 61).any()  # points were pruned: prune draws between plans
+    assert_rows_equal(points_rows(pts), read_dump(tmp / "o.dump"), f"plan {variant}")
+    assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
+    assert st["plan_mode"] == (variant != "rows")
+    assert (st["plan_fallback"] > 0) == (variant == "fallback")
+
+
+@pytest.mark.parametrize("variant", ["pool", "pool_copy", "pool_fallback"])
+def test_two_ranks_plan_mode_match_oracle(built, tmp, variant):
+    """Plan mode with one process per GPU (two ranks on GPU 0, shared-memory exchange): the node
+    leader publishes each trial's plan in the shared pool and both ranks' devices apply it
+    ("pool_copy": the plan copied into each rank's own pinned staging; "pool_fallback": no plan fits,
+    the leader publishes a marker and every rank builds the rows from its own rand() stream)."""
+    snp, opts = _windowed_genome(tmp, seed=94)
+    run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29700 + os.getpid() % 1000), WORLD_SIZE="2",
+               FSCL_AMD_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0", FSCL_AMD_RANK_TIMEOUT="120",
+               FSCL_MR_SHM=f"/fscl_amd_mrp_{os.getpid()}")
+    if variant == "pool_copy":
+        env["FSCL_AMD_POOL_COPY"] = "1"
+    if variant == "pool_fallback":
+        env["FSCL_AMD_PLAN_ECAP"] = "1"
+    procs = [subprocess.Popen([sys.executable, str(ROOT / "tests" / "mr_worker.py"), str(snp), str(tmp / f"o{r}.txt"),
+                               *opts], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for r in range(2)]
+    errs = []
+    for p in procs:
+        _, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err
+        errs.append(err)
+    assert (tmp / "o0.txt").read_text() == (tmp / "o.txt").read_text()
+    for e in errs:
+        assert "plan_mode 1" in e and "perm_leader 1" in e, e[-400:]
+        assert ("plan_fallback 0" in e) == (variant != "pool_fallback"), e[-400:]
 
 
 def test_pipelined_trials_match_lockstep_and_oracle(built, tmp, monkeypatch):

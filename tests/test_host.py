@@ -549,3 +549,40 @@ def test_block_plan_is_the_sequential_block_permutation(built, geom):
         assert negj == st[5]
     if n < 10_000:  # the edge cases this geometry is there for
         assert negj > 0 and rot > 0, (negj, rot)
+
+
+def test_bench_line_assembly_from_recorded_stats(built, monkeypatch):
+    """bench.py's JSON line (roofline with the committed profile, the stats block, cpu_baseline with
+    its anchor) assembled on the CPU from a recorded stats dict: a missing stats field or a key error
+    in the line's assembly fails here, not after minutes of GPU time (VERDICT r04 weak #8)."""
+    import argparse
+    import json as _json
+    import bench
+    rec = _json.loads((ROOT / "profiles" / "r04z_bench_c4.json").read_text().strip().splitlines()[-1])
+    st = fscl_amd.Stats().as_dict()
+    st.update({k: v for k, v in rec["stats"].items() if k in st})
+    st.update(kernel_ms=11617.0, n_launches=4002, busy_ms=5349.0, n_dup_cells=1, n_ep_saved=2, negj=26)
+    args = argparse.Namespace(config="C4", chromosomes=None, profile_summary=None, steps=2, warmup=1,
+                              permute_mode="parity", exchange="shm", cpu_threads=None, cpu_sample=None,
+                              cpu_full_job=False, n_permute=None)
+    cfg = dict(synth.CONFIGS["C4"])
+    line = bench.bench_line(args, cfg, st, 2.2e6, 10.0, 1, 1, 1, 1000, 10010, 3.0)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "stats"):
+        assert k in line, k
+    roof = line["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "limiter", "source"):
+        assert k in roof, k
+    assert roof["source"] and roof["traffic"] and 0 < roof["frac"] < 2
+    assert line["stats"]["perm_leader"] == 0 and "plan_mode" in line["stats"]
+    canned = {"sample_cells": 384.0, "threads": 16.0, "cell_s": 2.0, "perm_gen_s": 0.003, "perm_cells": 384.0,
+              "perm_cell_s": 2.1}
+    monkeypatch.setattr(bench, "_harness", lambda snp, cfg, threads, n: dict(canned))
+    info = bench.cpu_info()
+    bl, d, m = bench.cpu_baseline(args, cfg, None, None, info, fscl_amd, None, None, 10010, 1_170_000, 1001, 1.18e6,
+                                  5.4, live_parity=False)
+    for k in ("value", "unit", "cores", "kind", "sample", "threads_1", "node_linear", "anchor"):
+        assert k in bl, k
+    assert bl["anchor"]["source"].startswith("profiles/") and 0.5 < bl["anchor"]["measured_over_extrapolated"] < 2
+    line["cpu_baseline"] = bl
+    _json.dumps(line)

@@ -106,6 +106,38 @@ def test_shared_memory_allgather(built, tmp_path, world):
         assert "ok" in out.split(), out
 
 
+def test_stale_segment_of_a_dead_launch_is_replaced(built, tmp_path):
+    """A launch whose rank 0 died before every rank attached leaves its segment (rank 0 unlinks the
+    name only once all have attached).  The CLI's default name repeats across launches of one
+    launcher, so the next launch's rank 0 removes a segment whose creator is gone, and
+    its other ranks skip it: the ranks meet."""
+    import signal
+    import time
+    script = tmp_path / "s.py"
+    script.write_text(SHM_WORKER)
+    name = f"/fscl_amd_test_stale_{os.getpid()}"
+    env = dict(os.environ, WORLD_SIZE="2", REPO=str(ROOT), SHM_NAME=name, FSCL_AMD_RANK_TIMEOUT="60")
+    dead = subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK="0"), stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)  # waits for a rank 1 that never comes
+    t0 = time.time()
+    while not os.path.exists("/dev/shm" + name) and time.time() - t0 < 60:
+        time.sleep(0.05)
+    time.sleep(0.5)
+    dead.send_signal(signal.SIGKILL)
+    dead.communicate(timeout=60)
+    assert os.path.exists("/dev/shm" + name)  # the stale segment
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in (1, 0)]  # rank 1 first: it must skip it
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=300)
+            assert p.returncode == 0, err
+            assert "ok" in out.split(), out
+    finally:
+        if os.path.exists("/dev/shm" + name):
+            os.unlink("/dev/shm" + name)
+
+
 def test_device_shares_are_contiguous_and_cover(built):
     """world * n_dev shares (rank r's local device l takes share r * n_dev + l): consecutive,
     disjoint, covering, and each rank's devices form one contiguous range."""
