@@ -524,7 +524,8 @@ def bench_line(args, cfg: dict, st: dict, units: float, elapsed: float, n_gpus: 
                                      "host_null_s", "host_upload_s", "search_s", "prune_s", "n_dup_cells",
                                      "n_ep_saved", "wait_s", "n_crit", "n_drain", "spec_threads", "spec_posted",
                                      "spec_hits", "spec_cands", "spec_wait_s", "spec_done", "spec_gen_s",
-                                     "spec_claimed", "n_merged", "perm_leader", "plan_mode", "plan_fallback")},
+                                     "spec_claimed", "n_merged", "perm_leader", "plan_mode", "plan_fallback",
+                                     "spec_rank")},
     }
 
 

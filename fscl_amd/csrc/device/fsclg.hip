@@ -148,6 +148,8 @@ struct Params {
   int off_thr, off_nul;        // byte offsets in fsclg_dyn (the coefficient window at 0)
   int off_lt, lt_hi;           // LDS copy of logt3 branch 2 (|d| > 2^24) entries [256, lt_hi) at off_lt; lt_hi 0: none
   uint32_t lt_span;            // |d| is in that copy iff |d| - 2^24 < lt_span (unsigned); 0: none
+  const double* lx;            // FSCLG_LOG_CALC: the mid branch computed (logx_mid), its 256-entry table (LX_BYTES)
+  int off_lx, lx_on;           //   at off_lx in LDS; lx_on 0: the mid branch from logt3 (the device check failed)
   int eval_range;
   int bp_resl;
   int n_cells;
@@ -300,6 +302,49 @@ __device__ __forceinline__ double logt_lds(uint32_t ad, const Params& P) {
       return reinterpret_cast<const double*>(fsclg_dyn + P.off_lt)[i2];  // off_lt is pre-offset by -256 entries
   }
   return logt_dev(ad, P.logt3);
+}
+
+// FSCLG_LOG_CALC: the mid branch of logt (sm-search.c:43: 5.545177444479562 + log_table[|d| >> 8],
+// i = |d| >> 8 in [256, 65536)) computed instead of gathered from the 512 KB table.  i = 2^e m,
+// m = i << (15 - e) in [2^15, 2^16); c = the top 9 bits of m (256 choices, k), r = (m - c) / c
+// with |r| < 2^-8: log(i) = log(c) - (15 - e) ln2 + log1p(r), log(c) tabulated as hi + lo,
+// (15 - e) ln2_hi exact (42-bit ln2_hi), log1p(r) = r - r^2/2 + r^3 (1/3 - r/4 + r^2/5 - r^3/6).
+// The host evaluates the same operations for all 65 280 i against the reference's table
+// (logx_table: glibc's log, the same IEEE add), adjusts the lo parts of the few k whose entries
+// round the other way, and the device checks every entry once (logx_check_kernel): every
+// value is the table's, bit for bit, or the path stays off.
+constexpr int LX_BYTES = 256 * 32;  // per k: log(c) hi, lo, RN(1/c), pad
+constexpr double LX_LN2_HI = 0x1.62e42fefa38p-1, LX_LN2_LO = 0x1.ef35793c7673p-45;
+__host__ __device__ __forceinline__ double logx_mid(uint32_t i, const double* lx) {
+  const int e = 31 - __builtin_clz(i);
+  const int n = 15 - e;
+  const uint32_t m = i << n;
+  const uint32_t k = (m >> 7) & 255u;
+  const double lch = lx[4 * k], lcl = lx[4 * k + 1], inv = lx[4 * k + 2];
+  const double f = (double)(m & 127u), dn = (double)n;
+  const double rh = f * inv;
+  const double A = __builtin_fma(-dn, LX_LN2_HI, lch);  // exact
+  const double q = __builtin_fma(-dn, LX_LN2_LO, lcl);
+  const double sh = A + rh;
+  const double t = (A - sh) + rh;
+  const double r2 = rh * rh;
+  double p = __builtin_fma(rh, -1.0 / 6, 1.0 / 5);
+  p = __builtin_fma(rh, p, -1.0 / 4);
+  p = __builtin_fma(rh, p, 1.0 / 3);
+  const double r3 = r2 * rh;
+  p = r3 * p;
+  double lo = t + q;
+  lo = __builtin_fma(-0.5, r2, lo);
+  lo = lo + p;
+  const double L = sh + lo;
+  return 5.545177444479562 + L;
+}
+
+// every mid-branch entry computed on the device against the uploaded table: mismatches counted
+__global__ void __launch_bounds__(256) logx_check_kernel(const double* __restrict__ lx, const double* __restrict__ lt3,
+                                                         unsigned long long* __restrict__ bad) {
+  const uint32_t i = 256u + blockIdx.x * 256u + threadIdx.x;
+  if (i < 0x10000u && logx_mid(i, lx) != lt3[0x10000u + i]) atomicAdd(bad, 1ull);
 }
 
 // |pos_i - sweep| from biased positions: one v_sad_u32
@@ -718,9 +763,18 @@ __device__ __forceinline__ void run_segment_idx(SM& S, int w, int s, int s1, con
 #pragma unroll
       for (int u = 0; u < U; u++) x[u] = lt2[ad[u] >> 16] + la;
     } else if (__builtin_amdgcn_ballot_w64(mid) == ~0ull) {
-      const char* lt1 = reinterpret_cast<const char*>(P.logt3 + 0x10000);
+#ifdef FSCLG_LOG_CALC
+      if (LDS && P.lx_on) {
+        const double* lx = reinterpret_cast<const double*>(fsclg_dyn + P.off_lx);
 #pragma unroll
-      for (int u = 0; u < U; u++) x[u] = *reinterpret_cast<const double*>(lt1 + ((ad[u] >> 8) << 3)) + la;
+        for (int u = 0; u < U; u++) x[u] = logx_mid(ad[u] >> 8, lx) + la;
+      } else
+#endif
+      {
+        const char* lt1 = reinterpret_cast<const char*>(P.logt3 + 0x10000);
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u] = *reinterpret_cast<const double*>(lt1 + ((ad[u] >> 8) << 3)) + la;
+      }
     } else {
 #pragma unroll
       for (int u = 0; u < U; u++) x[u] = logt_lds<LDS>(ad[u], P) + la;
@@ -1465,6 +1519,12 @@ __device__ __forceinline__ void maxpos_body(SM& S, const Params& P) {
     load_window(S, P, P.ivc0);
     double* lt2 = reinterpret_cast<double*>(fsclg_dyn + P.off_lt);
     for (int j = 256 + tid; j < P.lt_hi; j += WG) lt2[j] = P.logt3[2 * 0x10000 + j];
+#ifdef FSCLG_LOG_CALC
+    if (P.lx_on) {
+      double* lx = reinterpret_cast<double*>(fsclg_dyn + P.off_lx);
+      for (int j = tid; j < LX_BYTES / 8; j += WG) lx[j] = P.lx[j];
+    }
+#endif
   } else if (tid == 0) S.ivc0 = 0;
   __syncthreads();
   if (P.mode == 1) {
@@ -2043,6 +2103,8 @@ struct fsclg_ctx {
   hipEvent_t wev0, wev1;          // window null-sum kernel timing
   // tables
   double* d_logt = nullptr;
+  double* d_lx = nullptr;         // FSCLG_LOG_CALC: logx_mid's table (LX_BYTES)
+  int lx_on = 0;
   double* d_coef = nullptr;
   double* d_null = nullptr;
   double* d_thr = nullptr;
@@ -2212,7 +2274,7 @@ int fsclg_close(fsclg_ctx* c) {
   hipDeviceSynchronize();
   void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0,
                   c->d_chr_start, c->d_chr_n, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine,
-                  c->d_stats, c->d_dfail, c->d_plan_tmp};
+                  c->d_stats, c->d_dfail, c->d_plan_tmp, c->d_lx};
   for (void* p : ptrs) if (p) hipFree(p);
   for (Slot& S : c->slot) {
     for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null, (void*)S.d_ctab, (void*)S.d_ctree})
@@ -2246,6 +2308,63 @@ static bool any_pending(const fsclg_ctx* c) {
   return false;
 }
 
+#ifdef FSCLG_LOG_CALC
+// logx_mid's table: per k, log(c) as hi + lo (long double) and RN(1/c); then every entry of the
+// mid branch evaluated here with the device's operations, and the lo part of a k whose entries
+// do not all reproduce the reference's table shifted (in 2^-68 steps, up to 2^-59) until they do;
+// then the device's own evaluation checked once against the uploaded table.  Any entry still
+// off: the mid branch keeps the gather (lx_on 0).
+static int logx_setup(fsclg_ctx* c, const std::vector<double>& lt3) {
+  std::vector<double> lx(LX_BYTES / 8, 0.0);
+  for (int k = 0; k < 256; k++) {
+    const double cc = (256.0 + k) * 128.0;
+    const long double lc = logl((long double)cc);
+    lx[4 * k] = (double)lc;
+    lx[4 * k + 1] = (double)(lc - (long double)lx[4 * k]);
+    lx[4 * k + 2] = 1.0 / cc;
+  }
+  auto k_of = [](uint32_t i) { return ((i << (15 - (31 - __builtin_clz(i)))) >> 7) & 255u; };
+  auto k_ok = [&](uint32_t k) {
+    for (uint32_t i = 256; i < 0x10000u; i++)
+      if (k_of(i) == k && logx_mid(i, lx.data()) != lt3[0x10000u + i]) return false;
+    return true;
+  };
+  std::vector<char> bad_k(256, 0);
+  for (uint32_t i = 256; i < 0x10000u; i++)
+    if (logx_mid(i, lx.data()) != lt3[0x10000u + i]) bad_k[k_of(i)] = 1;
+  bool ok = true;
+  for (int k = 0; k < 256 && ok; k++) {
+    if (!bad_k[k]) continue;
+    const double base = lx[4 * k + 1];
+    bool fixed = false;
+    for (int t = 1; t <= 512 && !fixed; t++)
+      for (int sg = -1; sg <= 1 && !fixed; sg += 2) {
+        lx[4 * k + 1] = base + sg * t * 0x1p-68;
+        fixed = k_ok((uint32_t)k);
+      }
+    if (!fixed) { lx[4 * k + 1] = base; ok = false; }
+  }
+  c->lx_on = 0;
+  if (!ok) return FSCLG_OK;
+  int r;
+  if ((r = upload(&c->d_lx, lx.data(), lx.size(), c->ustream))) return r;
+  unsigned long long* d_bad = nullptr;
+  unsigned long long bad = 1;
+  HIPCHK(hipMalloc((void**)&d_bad, sizeof bad), "hipMalloc");
+  HIPCHK(hipMemsetAsync(d_bad, 0, sizeof bad, c->ustream), "hipMemsetAsync");
+  hipLaunchKernelGGL(logx_check_kernel, dim3((0x10000 - 256 + 255) / 256), dim3(256), 0, c->ustream, c->d_lx, c->d_logt,
+                     d_bad);
+  HIPCHK(hipGetLastError(), "launch logx_check_kernel");
+  HIPCHK(hipMemcpyAsync(&bad, d_bad, sizeof bad, hipMemcpyDeviceToHost, c->ustream), "hipMemcpyAsync");
+  HIPCHK(hipStreamSynchronize(c->ustream), "hipStreamSynchronize");
+  hipFree(d_bad);
+  c->lx_on = bad == 0 && !getenv("FSCLG_NO_LOGX");
+  if (bad) fprintf(stderr, "fsclg: the device's mid-branch log distances differ from the table in %llu entries: "
+                           "the table is gathered instead\n", bad);
+  return FSCLG_OK;
+}
+#endif
+
 int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coef, int n_rows, int n_iv,
                         const double* nullrow, double log_ad_step) {
   if (!c || !log_table || !coef || !nullrow || n_rows <= 0 || n_iv <= 0) return set_err(FSCLG_E_ARG, "tables");
@@ -2264,6 +2383,9 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
       lt3[(size_t)b * 0x10000 + i] = b ? (double)v : log_table[i];
     }
   if ((r = upload(&c->d_logt, lt3.data(), lt3.size(), c->ustream))) return r;
+#ifdef FSCLG_LOG_CALC
+  if ((r = logx_setup(c, lt3))) return r;
+#endif
   c->h_lt3.swap(lt3);
   if ((r = update_dfail(c))) return r;
   // [row][iv][4] -> [iv][plane][1 + row][2] (coef_off): device row 0 is an all-zero sentinel
@@ -2928,7 +3050,8 @@ static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, 
 static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
   c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
-  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0);
+  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0) -
+                   (c->lx_on ? LX_BYTES + 16 : 0);
   double htot = 0.0;
   for (double h : hist) htot += h;
   if (room < 32 || htot <= 0) return;
@@ -2960,7 +3083,8 @@ static void plan_cache(fsclg_ctx* c) {
   c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
   if (getenv("FSCLG_NO_WINDOW")) return;  // experiment: every coefficient from the global table
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
-  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0);
+  const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0) -
+                   (c->lx_on ? LX_BYTES + 16 : 0);
   if (room < 32 || c->n_iv <= 0 || c->h_pos.empty() || c->h_coarse.empty() || c->h_lt3.empty()) return;
   std::vector<double> hist(c->n_iv, 0.0);
   std::vector<double> las(c->h_coarse);
@@ -3005,6 +3129,8 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.off_thr = P.n_cache * 32; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
   P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8; P.lt_hi = c->lt_hi;  // entry i at off_lt + 8 i
   P.lt_span = c->lt_hi > 256 ? ((uint32_t)c->lt_hi << 16) - 0x1000000u : 0u;  // lt_hi <= 32768
+  P.lx = c->d_lx; P.lx_on = c->lx_on;
+  P.off_lx = (P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0) + 15) & ~15;
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = S.d_chr_null; P.win_null = S.d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.dfail = c->d_dfail;
@@ -3068,7 +3194,7 @@ static int launch_blocks(hipStream_t stream, const Params& P, int n) {
 }
 static int launch_blocks_impl(hipStream_t stream, const Params& P, int n) {
   const int grid = n;
-  const int dyn = P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
+  const int dyn = P.lx_on ? P.off_lx + LX_BYTES : P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
   const int stat_m = (int)((sizeof(Smem) + 15) / 16 * 16), stat_s = (int)((sizeof(SmemSplit) + 15) / 16 * 16);
   if ((P.split > 1 ? stat_s : stat_m) + dyn <= LDS_WG) {
     static unsigned long long attr_set = 0;  // per device (bit = device id)

@@ -1146,6 +1146,7 @@ static int spec_take(int d, fh_rand_t *g) {
   int c, hit = -1, bi = -1;
   pthread_mutex_lock(&SP.mu);
   for (c = 0; c < SP.n_job; c++) if (SP.d[c] == d) hit = c;
+  if (hit >= 0) D.st.spec_rank[hit < 7 ? hit : 7]++;  /* the draw count's rank among the candidates posted */
   if (hit >= 0 && SP.state[hit] == 0) {
     /* not started (the workers are still on likelier ones): building it here is faster than
        waiting for a worker to get to it; the caller builds it (its buffer is freed below) */
@@ -1379,7 +1380,7 @@ static int spec_candidates(const scan_t *s, const pqueue_t *pq, const trial_batc
 }
 
 /* plan mode for this permute_pipelined call (PM.on): only when no chromosome's whole-chromosome
-   null sum is read (the host never needs the permuted rows) and a plan is smaller than the rows;
+   null sum is read (the host never needs the permuted rows);
    the buffers are sized from one plan drawn from a copy of the stream (every rank draws the same).
    FSCL_AMD_PLAN=0: never; FSCL_AMD_PLAN_ECAP=m (tests): buffers of m entries, so that a plan can
    fail to fit and the trial falls back to rows built on the host */
@@ -1402,7 +1403,17 @@ static int plan_mode_setup(double nbp, double width_mb, const fh_rand_t *g) {
   if (ec) PM.ecap = atoi(ec) > 0 ? atoi(ec) : 1;
   PM.bytes = sizeof(plan_hdr_t) + ((sizeof(int32_t) * (size_t)(PM.gcap + 1) + 15) & ~(size_t)15) +
              sizeof(fsclg_swap_t) * (size_t)PM.ecap;
-  return PM.bytes <= (size_t)D.rb * (size_t)n;
+  if (PM.bytes > (size_t)D.rb * (size_t)D.stage_cap) {  /* small genomes: the slots' staging holds a plan too */
+    const int cap = (int)((PM.bytes + (size_t)D.rb - 1) / (size_t)D.rb);
+    int k;
+    for (k = 0; k < FSCLG_N_SLOTS; k++) {
+      fsclg_host_free(D.stage[k]);
+      D.stage[k] = fsclg_host_alloc((size_t)D.rb * (size_t)cap);
+      if (!D.stage[k]) logmsg(MSG_FATAL, "fscl_amd: row staging: %s", fsclg_last_error());
+    }
+    D.stage_cap = cap;
+  }
+  return 1;
 }
 
 static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eval_range, int bp_resl,
@@ -1482,6 +1493,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
         block_permute(D.stage[slot], D.rowp, s->n_snps, permute_nbp, scan_width_mb, &g0, &nj2, NULL, 0);
         if (memcmp(&g0, g, sizeof g0) != 0 || nj2 != nj) logmsg(MSG_FATAL, "fscl_amd: permutation pool: stream mismatch");
         rows_here = 1;
+        D.st.plan_fallback++;
       }
       D.st.negj += nj;
     } else {

@@ -238,6 +238,8 @@ typedef struct {
   int plan_mode;          /* scan_permute: 1 if the trials' permutations went to the devices as plans
                              (fsclg_slot_set_rows_plan), 0 as rows */
   unsigned long long plan_fallback; /* plan mode: trials whose plan did not fit its buffer (rows instead) */
+  unsigned long long spec_rank[8];  /* speculation hits by the candidate's rank in the likeliest-first order
+                                       (7: rank 7 or later): how many launched-ahead candidates would cover */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);
