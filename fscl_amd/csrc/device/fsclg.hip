@@ -3445,6 +3445,7 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
     P.ivc0 = 0; P.n_civ = 0; P.civ_max = 0; P.n_cache = 0;
     P.off_thr = 0; P.off_nul = (c->n_iv + 1) * 8;
     P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8;
+    P.off_lx = (P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0) + 15) & ~15;
   }
   if ((r = launch_blocks(B.stream, P, G > 1 ? (nl + 7) / 8 * 8 * G : nl))) return r;
   HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");
@@ -3595,6 +3596,7 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
     P.ivc0 = 0; P.n_civ = 0; P.civ_max = 0; P.n_cache = 0;  // as a split batch: no LDS coefficient windows
     P.off_thr = 0; P.off_nul = (c->n_iv + 1) * 8;
     P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8;
+    P.off_lx = (P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0) + 15) & ~15;
   }
   HIPCHK(hipEventRecord(B.ev0, B.stream), "hipEventRecord");
   if ((r = launch_blocks(B.stream, P, G > 1 ? (n_pts + 7) / 8 * 8 * G : n_pts))) return r;

@@ -502,7 +502,7 @@ static struct {
   int32_t *ext;        /* fh_ext_table of D's sites for ext_width */
   double ext_width;
   int ext_n;
-  const void *ext_key;
+  uint64_t ext_key;    /* D.key (the sites' content hash) the table was built for */
   fh_perm_geom_t G;
   int on;              /* plan mode in the current permute_pipelined call */
   int ecap, gcap;      /* a plan buffer's capacity: entries, groups */
@@ -510,11 +510,11 @@ static struct {
 } PM;
 
 static void perm_geom(double width_mb) {
-  if (!PM.ext || PM.ext_n != D.n_snps_key || PM.ext_width != width_mb || PM.ext_key != (const void *)D.pos) {
+  if (!PM.ext || PM.ext_n != D.n_snps_key || PM.ext_width != width_mb || PM.ext_key != D.key) {
     free(PM.ext);
     PM.ext = fh_malloc(sizeof(int32_t) * (size_t)(D.n_snps_key ? D.n_snps_key : 1), "extension table");
     fh_ext_table(PM.ext, D.pos, D.chr_start, D.chr_n, D.n_chr, width_mb);
-    PM.ext_n = D.n_snps_key; PM.ext_width = width_mb; PM.ext_key = D.pos;
+    PM.ext_n = D.n_snps_key; PM.ext_width = width_mb; PM.ext_key = D.key;
   }
   PM.G.n = D.n_snps_key; PM.G.n_chr = D.n_chr; PM.G.chr_start = D.chr_start; PM.G.chr_n = D.chr_n;
   PM.G.pos = D.pos; PM.G.ext = PM.ext;

@@ -379,6 +379,20 @@ def test_two_ranks_plan_mode_match_oracle(built, tmp, variant):
         assert ("plan_fallback 0" in e) == (variant != "pool_fallback"), e[-400:]
 
 
+def test_block_extension_table_follows_the_genome(built, tmp):
+    """Two genomes of the same size one after the other in one process (the per-site extension
+    table of the block permutation, perm.c, is keyed by the sites' content, not by where they
+    happen to be allocated): both permutation tests bit-identical to the oracle."""
+    for seed in (71, 72):
+        snp = tmp / f"ext{seed}.snp"
+        synth.write_snp_file(str(snp), synth.generate(n_chr=2, chr_len=8_000_000, snps_per_chr=8000, n=30, seed=seed,
+                                                      sweeps_per_chr=2))
+        opts = ["--coarse-grid-spacing=40000", "--n-permute=30"]
+        run_oracle(snp, tmp / f"o{seed}.txt", opts, tmp / f"o{seed}.dump")
+        scan = fscl_amd.run(snp, tmp / f"g{seed}.txt", **_kw(opts))
+        assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / f"o{seed}.dump"), f"genome {seed}")
+
+
 def test_pipelined_trials_match_lockstep_and_oracle(built, tmp, monkeypatch):
     """Two trials in flight (scan_permute's default): the rand-stream critical points
     (permute_p >= 19) run ahead of the rest of their trial, the next trial's permutation is

@@ -42,7 +42,7 @@ run() {  # <name> <burners> <round> [env ...]: the replay sizes its threads as t
   local rc=$?
   unburn
   [ $rc -eq 0 ] || exit 1
-  echo "$1 ($2 busy CPUs beside; ${@:4}) round $3: $(python3 -c "import json;d=json.load(open('$OUT/w${W}_$1_$3.json'));s=d['stats'];print(round(d['ms_per_step']), 'ms/job; blocked on batches', round(s['wait_s'],3), 's; spec threads', s['spec_threads'], 'hits', s['spec_hits'], '/', s['trials'], 'claimed', s.get('spec_claimed'), 'wait', round(s['spec_wait_s'],3), 's; main-thread perm', round(s['host_perm_s'],3), 'null', round(s['host_null_s'],3), 's')")"
+  echo "$1 ($2 busy CPUs beside; ${@:4}) round $3: $(python3 -c "import json;d=json.load(open('$OUT/w${W}_$1_$3.json'));s=d['stats'];print(round(d['ms_per_step']), 'ms/job; blocked on batches', round(s['wait_s'],3), 's; spec threads', s['spec_threads'], 'hits', s['spec_hits'], '/', s['trials'], 'claimed', s.get('spec_claimed'), 'wait', round(s['spec_wait_s'],3), 's; main-thread perm', round(s['host_perm_s'],3), 'null', round(s['host_null_s'],3), 's; plan', s.get('plan_mode'), 'rank hist', s.get('spec_rank'))")"
 }
 PER=$((U / W)); [ $PER -lt 1 ] && PER=1
 for r in $(seq ${ROUNDS:-2}); do
@@ -50,7 +50,7 @@ for r in $(seq ${ROUNDS:-2}); do
     # <variant>@VAR=x,VAR2=y: the variant with extra environment (e.g. leader@FSCLG_SPLIT_BUDGET=512)
     v=${v0%%@*}; X=""; [ "$v" != "$v0" ] && X=${v0#*@}; X=${X//,/ }
     if [ -n "$X" ]; then
-      N=$(echo "${v}_$X" | tr ' =' '_-')
+      N=$(echo "${v}_${X##*/}" | tr ' =' '_-')
       case $v in
         single) run $N 0 $r LOCAL_WORLD_SIZE=1 FSCL_AMD_PERM_LEADER=0 $X ;;
         leader) run $N $((W - 1)) $r $X ;;
