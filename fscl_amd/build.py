@@ -106,9 +106,11 @@ def main(argv: list[str]) -> int:
         build_native(force=force, trace=True)
     if "--rehearsal" in argv:  # the scaling-rehearsal test build (tools/scale_sim.sh)
         build_native(force=force, variant="rehearsal", defines=("-DFSCL_AMD_REHEARSAL",))
-    if "--logx" in argv:  # the computed mid-branch log distance (FSCLG_LOG_CALC), and its rehearsal build
-        build_native(force=force, variant="logx", defines=("-DFSCLG_LOG_CALC",))
-        build_native(force=force, variant="rehearsal_logx", defines=("-DFSCL_AMD_REHEARSAL", "-DFSCLG_LOG_CALC"))
+    if "--logx" in argv:  # the computed mid-branch log distance (FSCLG_LOG_CALC): 2 in every
+        # kernel, 1 in the split kernel only; and their rehearsal builds
+        for v, lc in (("logx", "2"), ("logxs", "1")):
+            build_native(force=force, variant=v, defines=(f"-DFSCLG_LOG_CALC={lc}",))
+            build_native(force=force, variant=f"rehearsal_{v}", defines=("-DFSCL_AMD_REHEARSAL", f"-DFSCLG_LOG_CALC={lc}"))
     if "--no-oracle" not in argv:
         build_oracle()
     return 0

@@ -314,6 +314,13 @@ __device__ __forceinline__ double logt_lds(uint32_t ad, const Params& P) {
 // round the other way, and the device checks every entry once (logx_check_kernel): every
 // value is the table's, bit for bit, or the path stays off.
 constexpr int LX_BYTES = 256 * 32;  // per k: log(c) hi, lo, RN(1/c), pad
+#ifndef FSCLG_LOG_CALC
+#define FSCLG_LOG_CALC 0
+#endif
+// FSCLG_LOG_CALC=1: in the split kernel only (the latency-bound tail); 2: in every kernel
+template <class SM> constexpr bool lx_kernel() {
+  return FSCLG_LOG_CALC >= 2 || (FSCLG_LOG_CALC == 1 && std::is_same<SM, SmemSplit>::value);
+}
 constexpr double LX_LN2_HI = 0x1.62e42fefa38p-1, LX_LN2_LO = 0x1.ef35793c7673p-45;
 __host__ __device__ __forceinline__ double logx_mid(uint32_t i, const double* lx) {
   const int e = 31 - __builtin_clz(i);
@@ -763,8 +770,8 @@ __device__ __forceinline__ void run_segment_idx(SM& S, int w, int s, int s1, con
 #pragma unroll
       for (int u = 0; u < U; u++) x[u] = lt2[ad[u] >> 16] + la;
     } else if (__builtin_amdgcn_ballot_w64(mid) == ~0ull) {
-#ifdef FSCLG_LOG_CALC
-      if (LDS && P.lx_on) {
+#if FSCLG_LOG_CALC
+      if (LDS && lx_kernel<SM>() && P.lx_on) {
         const double* lx = reinterpret_cast<const double*>(fsclg_dyn + P.off_lx);
 #pragma unroll
         for (int u = 0; u < U; u++) x[u] = logx_mid(ad[u] >> 8, lx) + la;
@@ -1519,8 +1526,8 @@ __device__ __forceinline__ void maxpos_body(SM& S, const Params& P) {
     load_window(S, P, P.ivc0);
     double* lt2 = reinterpret_cast<double*>(fsclg_dyn + P.off_lt);
     for (int j = 256 + tid; j < P.lt_hi; j += WG) lt2[j] = P.logt3[2 * 0x10000 + j];
-#ifdef FSCLG_LOG_CALC
-    if (P.lx_on) {
+#if FSCLG_LOG_CALC
+    if (lx_kernel<SM>() && P.lx_on) {
       double* lx = reinterpret_cast<double*>(fsclg_dyn + P.off_lx);
       for (int j = tid; j < LX_BYTES / 8; j += WG) lx[j] = P.lx[j];
     }
@@ -2308,7 +2315,7 @@ static bool any_pending(const fsclg_ctx* c) {
   return false;
 }
 
-#ifdef FSCLG_LOG_CALC
+#if FSCLG_LOG_CALC
 // logx_mid's table: per k, log(c) as hi + lo (long double) and RN(1/c); then every entry of the
 // mid branch evaluated here with the device's operations, and the lo part of a k whose entries
 // do not all reproduce the reference's table shifted (in 2^-68 steps, up to 2^-59) until they do;
@@ -2383,7 +2390,7 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
       lt3[(size_t)b * 0x10000 + i] = b ? (double)v : log_table[i];
     }
   if ((r = upload(&c->d_logt, lt3.data(), lt3.size(), c->ustream))) return r;
-#ifdef FSCLG_LOG_CALC
+#if FSCLG_LOG_CALC
   if ((r = logx_setup(c, lt3))) return r;
 #endif
   c->h_lt3.swap(lt3);
@@ -3051,7 +3058,7 @@ static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
   c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0) -
-                   (c->lx_on ? LX_BYTES + 16 : 0);
+                   (c->lx_on && FSCLG_LOG_CALC >= 2 ? LX_BYTES + 16 : 0);
   double htot = 0.0;
   for (double h : hist) htot += h;
   if (room < 32 || htot <= 0) return;
@@ -3084,7 +3091,7 @@ static void plan_cache(fsclg_ctx* c) {
   if (getenv("FSCLG_NO_WINDOW")) return;  // experiment: every coefficient from the global table
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0) -
-                   (c->lx_on ? LX_BYTES + 16 : 0);
+                   (c->lx_on && FSCLG_LOG_CALC >= 2 ? LX_BYTES + 16 : 0);
   if (room < 32 || c->n_iv <= 0 || c->h_pos.empty() || c->h_coarse.empty() || c->h_lt3.empty()) return;
   std::vector<double> hist(c->n_iv, 0.0);
   std::vector<double> las(c->h_coarse);
@@ -3129,7 +3136,7 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.off_thr = P.n_cache * 32; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
   P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8; P.lt_hi = c->lt_hi;  // entry i at off_lt + 8 i
   P.lt_span = c->lt_hi > 256 ? ((uint32_t)c->lt_hi << 16) - 0x1000000u : 0u;  // lt_hi <= 32768
-  P.lx = c->d_lx; P.lx_on = c->lx_on;
+  P.lx = c->d_lx; P.lx_on = FSCLG_LOG_CALC >= 2 ? c->lx_on : 0;  // FSCLG_LOG_CALC=1: set for split launches
   P.off_lx = (P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0) + 15) & ~15;
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = S.d_chr_null; P.win_null = S.d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
@@ -3302,7 +3309,10 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
   // resident together while other batches run (their workgroups never wait on anything)
   int G = 1;
   if (B.split_max > 1) {
-    static const int budget = getenv("FSCLG_SPLIT_BUDGET") ? atoi(getenv("FSCLG_SPLIT_BUDGET")) : 256;
+    // 512 (round 5): at 8 GPUs C5's tail batches of ~69 cells get 7 members instead of 3 (the rank-0
+    // rehearsal 59.7 -> 47.3 s per job, profiles/r05d_c5_ranks); batches of more than 256 cells (every
+    // one-GPU job's blocking batches but C5 chr1's) stay unsplit as before
+    static const int budget = getenv("FSCLG_SPLIT_BUDGET") ? atoi(getenv("FSCLG_SPLIT_BUDGET")) : 512;
     G = std::min(std::min(B.split_max, MAXSPLIT), budget / std::max(nu, 1));
     if (G < 2) G = 1;
   }
@@ -3446,6 +3456,7 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
     P.off_thr = 0; P.off_nul = (c->n_iv + 1) * 8;
     P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8;
     P.off_lx = (P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0) + 15) & ~15;
+    P.lx_on = FSCLG_LOG_CALC >= 1 ? c->lx_on : 0;
   }
   if ((r = launch_blocks(B.stream, P, G > 1 ? (nl + 7) / 8 * 8 * G : nl))) return r;
   HIPCHK(hipEventRecord(B.ev1, B.stream), "hipEventRecord");

@@ -1574,7 +1574,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       pq[a].n++;
     }
     /* a small bulk batch joins the blocking batch when the blocking batch's cells keep their full
-       split (8 members within the launch's 256-workgroup budget): the
+       split (8 members within 256 workgroups, half the launch budget, HISTORY.md §11.11): the
        early-prune tail's few bulk cells -- the most significant points, which never reach the
        blocking class -- would otherwise run one workgroup per cell and hold up the host K trials
        later.  Merged in ascending point order (the blocking batch's draws go in that order; the

@@ -184,9 +184,10 @@ int fsclg_set_alpha_grid(fsclg_ctx *c, const double *coarse, int n_coarse, const
 
 /* Split cells: a launch of batch `batch` with few cells gives each cell up to max_members
    (<= 8) workgroups that share its walks' segments (default 1).  For latency, not throughput:
-   the pipeline's blocking batch, whose result orders the next trial.  The members of a cell
-   are resident together (a budget of 256 workgroups per launch, below the device's resident
-   slots); a cell whose members were not fails with FSCLG_E_KERNEL. */
+   the pipeline's blocking batch, whose result orders the next trial.  A launch takes at most
+   512 workgroups ($FSCLG_SPLIT_BUDGET), the device's resident slots, so the members of a cell
+   run together once the workgroups ahead of them finish; a cell whose members were not all
+   resident within ~1 s is re-run with one workgroup (counted, n_split_retry). */
 int fsclg_set_batch_split(fsclg_ctx *c, int batch, int max_members);
 
 /* batched search_maxpos over n_cells cells; blocks until out[] is written */
