@@ -15,11 +15,19 @@ Path(dst).parent.mkdir(parents=True, exist_ok=True)
 if (src / "trace" / "run_kernel_stats.csv").exists():
     shutil.copy(src / "trace" / "run_kernel_stats.csv", f"{dst}_kernel_stats.csv")
 out = {"kernel": "search_maxpos_kernel"}
-for row in (csv.DictReader(open(src / "trace" / "run_kernel_stats.csv")) if (src / "trace" / "run_kernel_stats.csv").exists() else []):
-    if "search_maxpos" in row["Name"]:
-        out["trace"] = {"calls": int(row["Calls"]), "avg_ms": float(row["AverageNs"]) / 1e6,
-                        "min_ms": float(row["MinNs"]) / 1e6, "max_ms": float(row["MaxNs"]) / 1e6,
-                        "share_pct": float(row["Percentage"])}
+# every search_maxpos launch, one workgroup per cell or split (the hot path's two instantiations; bench.py's
+# HIP events count both alike)
+rows = [r for r in (csv.DictReader(open(src / "trace" / "run_kernel_stats.csv"))
+                    if (src / "trace" / "run_kernel_stats.csv").exists() else []) if "search_maxpos" in r["Name"]]
+if rows:
+    calls = sum(int(r["Calls"]) for r in rows)
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    out["trace"] = {"calls": calls, "avg_ms": tot / calls / 1e6,
+                    "min_ms": min(float(r["MinNs"]) for r in rows) / 1e6,
+                    "max_ms": max(float(r["MaxNs"]) for r in rows) / 1e6,
+                    "share_pct": sum(float(r["Percentage"]) for r in rows),
+                    "by_kernel": {("search_maxpos_split_kernel" if "split" in r["Name"] else "search_maxpos_kernel"):
+                                  int(r["Calls"]) for r in rows}}
 # launches of different batch streams overlap: the GPU time they occupy is the union of
 # their intervals (bench.py divides by the same union, measured with HIP events)
 kt = src / "trace" / "run_kernel_trace.csv"

@@ -38,7 +38,9 @@ while True: os.sched_yield()"
 unburn() { for p in $BURN_PIDS; do kill $p 2>/dev/null; done; wait $BURN_PIDS 2>/dev/null; BURN_PIDS=""; }
 run() {  # <name> <burners> <round> [env ...]: the replay sizes its threads as the product would for that env
   burn $2
-  env LOCAL_WORLD_SIZE=$W ${@:4} FSCL_AMD_SIM=replay:$REC:$W:0 timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w${W}_$1_$3.json 2> $OUT/w${W}_$1_$3.err
+  local P=""  # PROF=1: the replay under rocprofv3's kernel trace (per-kernel durations in $OUT/prof_<name>)
+  [ -n "$PROF" ] && P="rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$1_$3 -o run --"
+  (cd /tmp && env TMPDIR=/tmp LOCAL_WORLD_SIZE=$W ${@:4} FSCL_AMD_SIM=replay:$REC:$W:0 timeout -k 10 900 $P python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w${W}_$1_$3.json 2> $OUT/w${W}_$1_$3.err)
   local rc=$?
   unburn
   [ $rc -eq 0 ] || exit 1
