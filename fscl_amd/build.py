@@ -111,6 +111,10 @@ def main(argv: list[str]) -> int:
         for v, lc in (("logx", "2"), ("logxs", "1")):
             build_native(force=force, variant=v, defines=(f"-DFSCLG_LOG_CALC={lc}",))
             build_native(force=force, variant=f"rehearsal_{v}", defines=("-DFSCL_AMD_REHEARSAL", f"-DFSCLG_LOG_CALC={lc}"))
+    for a in argv:  # --variant=NAME:DEF[,DEF...]: an experiment build fscl_amd/_build_NAME with -DDEF each
+        if a.startswith("--variant="):
+            name, _, defs = a[len("--variant="):].partition(":")
+            build_native(force=force, variant=name, defines=tuple(f"-D{d}" for d in defs.split(",") if d))
     if "--no-oracle" not in argv:
         build_oracle()
     return 0

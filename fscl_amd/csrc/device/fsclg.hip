@@ -1763,35 +1763,54 @@ constexpr int WCG = 16;  // chunks per wave-uniform group (their table entries: 
 // choice of emin), so that the increment is fma(parity, d1 - d0, d0), exactly; NaN when the chunk holds a value that is positive, not finite, or lies past the last
 // site.  Binade-major, so that a group of consecutive chunks at one binade is one contiguous run;
 // nstride = chunks + WCG (the padding entries are NaN).
+#ifndef FSCLG_CT_BG
+#define FSCLG_CT_BG 8
+#endif
+constexpr int CT_BG = FSCLG_CT_BG;  // binades per thread: each chunk's 64 null values are read once per CT_BG binades
 __global__ void __launch_bounds__(256) chunk_table_kernel(const uint2* __restrict__ pr,
                                                           const double* __restrict__ nullrow, int n_snps, int emin,
                                                           int ne, int nstride, double2* __restrict__ tab) {
+  const int ng = (ne + CT_BG - 1) / CT_BG;
   const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= nstride * ne) return;
-  const int k = t / nstride, c = t - k * nstride;
-  const int e = emin + k;
+  if (t >= nstride * ng) return;
+  const int grp = t / nstride, c = t - grp * nstride, k0 = grp * CT_BG;
   const double nan = __longlong_as_double(0x7FF8000000000000ll);
-  if ((c + 1) * WC > n_snps) { tab[t] = make_double2(nan, nan); return; }
-  const double sc = __longlong_as_double((long long)(1023 + 52 - e) << 52);  // 2^(52 - e), e <= 52
-  long long d0 = 0, d1 = 0;
-  int p0 = 0, p1 = 1;
+  if ((c + 1) * WC > n_snps) {
+    for (int k = k0; k < ne && k < k0 + CT_BG; k++) tab[(size_t)k * nstride + c] = make_double2(nan, nan);
+    return;
+  }
+  // per binade e = emin + k: the running integer's increments from entry parity 0 and 1 (exact
+  // below 2^52: 64 values of magnitude < 2^e / 64 each, scaled by 2^(52 - e))
+  double d0[CT_BG], d1[CT_BG];
+  int p0[CT_BG], p1[CT_BG];
+#pragma unroll
+  for (int b = 0; b < CT_BG; b++) { d0[b] = 0.0; d1[b] = 0.0; p0[b] = 0; p1[b] = 1; }
   bool ok = true;
   for (int j = 0; j < WC; j++) {
     const double v = nullrow[pr[phys((uint32_t)(c * WC + j))].y];
     if (!(v <= 0.0) || v == -__builtin_inf()) { ok = false; break; }  // positive, NaN or -inf
-    const double q = v * sc;
-    const double F = floor(q);
-    const long long Fi = (long long)F;
-    if (q - F == 0.5) {
-      d0 += Fi + ((p0 + Fi) & 1); p0 = 0;
-      d1 += Fi + ((p1 + Fi) & 1); p1 = 0;
-    } else {
-      const long long R = (long long)rint(q);
-      d0 += R; p0 = (int)((p0 + R) & 1);
-      d1 += R; p1 = (int)((p1 + R) & 1);
+#pragma unroll
+    for (int b = 0; b < CT_BG; b++) {
+      const int e = emin + k0 + b;  // e <= 52 for the entries written; the others are computed and dropped
+      const double sc = __longlong_as_double((long long)(1023 + 52 - (e < 52 ? e : 52)) << 52);  // 2^(52 - e)
+      const double q = v * sc;
+      const double F = floor(q);
+      if (q - F == 0.5) {
+        const long long Fi = (long long)F;
+        d0[b] += (double)(Fi + ((p0[b] + Fi) & 1)); p0[b] = 0;
+        d1[b] += (double)(Fi + ((p1[b] + Fi) & 1)); p1[b] = 0;
+      } else {
+        const double R = rint(q);
+        const int Rp = (int)((long long)R & 1);
+        d0[b] += R; p0[b] = (p0[b] + Rp) & 1;
+        d1[b] += R; p1[b] = (p1[b] + Rp) & 1;
+      }
     }
   }
-  tab[t] = ok ? make_double2((double)d0, (double)(d1 - d0)) : make_double2(nan, nan);
+#pragma unroll
+  for (int b = 0; b < CT_BG; b++)
+    if (k0 + b < ne)
+      tab[(size_t)(k0 + b) * nstride + c] = ok ? make_double2(d0[b], d1[b] - d0[b]) : make_double2(nan, nan);
 }
 
 // Block maps.  Within one binade a chunk's increment depends on the running
@@ -1818,15 +1837,29 @@ __device__ __forceinline__ double2 compose_maps(double2 f1, double2 f2) {
   return make_double2(D0, D1 - D0);
 }
 
-// one block per binade: levels 1 .. lmax in turn (level L from level L - 1, level 0 the chunk table)
+// levels L0 .. L0 + nlev - 1 of the block maps, nlev <= CT_SPAN: each wave takes 64 consecutive
+// entries of level L0 - 1 (level 0: the chunk table) of one binade, one per lane, and composes them
+// level by level across its lanes (lane i holds the block starting at entry i once i is a multiple
+// of its size), writing each level's blocks that exist (block b of level L covers entries 2b,
+// 2b + 1 of level L - 1; level L has nb[L] = chunks >> L blocks).  No LDS, so the kernel runs
+// beside search workgroups that hold all of it; two launches cover 12 levels (ensure_ctab).
+constexpr int CT_SPAN = 6;
 __global__ void __launch_bounds__(256) chunk_tree_kernel(const double2* __restrict__ ctab, int nstride, CTree T,
-                                                         double2* __restrict__ out) {
-  const int k = blockIdx.x;
-  for (int L = 1; L <= T.lmax; L++) {
-    const double2* prev = L == 1 ? ctab + (size_t)k * nstride : out + T.off[L - 1] + (size_t)k * T.nb[L - 1];
-    double2* cur = out + T.off[L] + (size_t)k * T.nb[L];
-    for (int b = threadIdx.x; b < T.nb[L]; b += 256) cur[b] = compose_maps(prev[2 * b], prev[2 * b + 1]);
-    __syncthreads();  // the level's writes before the next level reads them (one workgroup)
+                                                         double2* __restrict__ out, int L0, int nlev, int ngrp) {
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x / ngrp, g = (blockIdx.x - k * ngrp) * 4 + (threadIdx.x >> 6);  // wave g of binade k
+  const int nprev = L0 == 1 ? nstride : T.nb[L0 - 1];
+  const double2* prev = L0 == 1 ? ctab + (size_t)k * nstride : out + T.off[L0 - 1] + (size_t)k * T.nb[L0 - 1];
+  const long long i0 = (long long)g * 64 + lane;
+  double2 v = i0 < nprev ? prev[i0] : make_double2(__longlong_as_double(0x7FF8000000000000ll), 0.0);
+  for (int l = 0; l < nlev; l++) {
+    const int st = 1 << l, L = L0 + l;
+    const double2 r = make_double2(__shfl_down(v.x, st, 64), __shfl_down(v.y, st, 64));
+    if ((lane & (2 * st - 1)) == 0) {
+      v = compose_maps(v, r);
+      const long long b = ((long long)g * 64 + lane) >> (l + 1);
+      if (b < T.nb[L]) out[T.off[L] + (size_t)k * T.nb[L] + b] = v;
+    }
   }
 }
 
@@ -2805,7 +2838,7 @@ static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne, long long W) {
     HIPCHK(hipMalloc((void**)&S.d_ctab, sizeof(double2) * need), "hipMalloc chunk table");
     S.ctab_cap = need;
   }
-  const long long nthr = (long long)nstride * ne;
+  const long long nthr = (long long)nstride * ((ne + CT_BG - 1) / CT_BG);
   hipLaunchKernelGGL(chunk_table_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, c->ustream, S.d_pr,
                      c->d_null, c->n_snps, emin, ne, nstride, S.d_ctab);
   HIPCHK(hipGetLastError(), "launch chunk_table_kernel");
@@ -2826,9 +2859,15 @@ static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne, long long W) {
       S.ctree_cap = tot;
     }
     S.ctree.p = S.d_ctree;
-    hipLaunchKernelGGL(chunk_tree_kernel, dim3((unsigned)ne), dim3(256), 0, c->ustream, S.d_ctab, nstride, S.ctree,
-                       S.d_ctree);
-    HIPCHK(hipGetLastError(), "launch chunk_tree_kernel");
+    for (int L0 = 1; L0 <= lmax; L0 += CT_SPAN) {  // levels L0 .. L0 + nlev - 1 per launch, from level L0 - 1
+      const int nlev = std::min(CT_SPAN, lmax - L0 + 1);
+      const int nprev = L0 == 1 ? nstride : S.ctree.nb[L0 - 1];
+      const int ngrp = (nprev + 255) / 256;  // four waves of 64 entries per workgroup
+      if (ngrp == 0) break;
+      hipLaunchKernelGGL(chunk_tree_kernel, dim3((unsigned)(ne * ngrp)), dim3(256), 0, c->ustream, S.d_ctab, nstride,
+                         S.ctree, S.d_ctree, L0, nlev, ngrp);
+      HIPCHK(hipGetLastError(), "launch chunk_tree_kernel");
+    }
   }
   S.ctab_valid = true; S.ctab_emin = emin; S.ctab_ne = ne;
   return FSCLG_OK;
