@@ -1837,6 +1837,77 @@ __device__ __forceinline__ double2 compose_maps(double2 f1, double2 f2) {
   return make_double2(D0, D1 - D0);
 }
 
+// The same table with the chunks' null values staged through LDS: a workgroup loads the 4096
+// values of 64 consecutive chunks with coalesced reads (one site per thread per pass) and stores them
+// transposed (tile[j][chunk], a row padded to 65 doubles), so that its four waves -- lane = chunk,
+// wave = a group of CT_BGL binades -- read their chunk's j-th value conflict-free.  chunk_table_kernel
+// reads each chunk's sites with one lane per chunk, 64 lanes 1 KB apart, per load.  A wave's 64
+// chunks are one aligned block of level 6, so it also composes the block maps of levels 1 .. nlev
+// (nlev <= CT_SPAN) across its lanes, as chunk_tree_kernel does, before anything is written back.
+constexpr int CT_BGL = 3;  // binades per lane per pass (4 waves x 3: C5's 12 binades in one pass)
+__global__ void __launch_bounds__(256) chunk_table_lds_kernel(const uint2* __restrict__ pr,
+                                                              const double* __restrict__ nullrow, int n_snps,
+                                                              int emin, int ne, int nstride,
+                                                              double2* __restrict__ tab, CTree T,
+                                                              double2* __restrict__ tree, int nlev) {
+  __shared__ double tile[WC][65];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c0 = blockIdx.x * 64;
+  const double nan = __longlong_as_double(0x7FF8000000000000ll);
+#pragma unroll 4
+  for (int q = 0; q < WC * 64 / 256; q++) {
+    const int k = q * 256 + t, sidx = c0 * WC + k;  // k: the block's k-th site, chunk k >> 6, index k & 63
+    tile[k & 63][k >> 6] = sidx < n_snps ? nullrow[pr[phys((uint32_t)sidx)].y] : nan;
+  }
+  __syncthreads();
+  const int c = c0 + lane;  // chunks past nstride: NaN, composed but never written
+  const bool whole = (c + 1) * WC <= n_snps;
+  for (int k0 = wave * CT_BGL; k0 < ne; k0 += 4 * CT_BGL) {
+    double d0[CT_BGL], d1[CT_BGL];
+    int p0[CT_BGL], p1[CT_BGL];
+#pragma unroll
+    for (int b = 0; b < CT_BGL; b++) { d0[b] = 0.0; d1[b] = 0.0; p0[b] = 0; p1[b] = 1; }
+    bool ok = whole;
+    for (int j = 0; j < WC && ok; j++) {
+      const double v = tile[j][lane];
+      if (!(v <= 0.0) || v == -__builtin_inf()) { ok = false; break; }  // positive, NaN or -inf
+#pragma unroll
+      for (int b = 0; b < CT_BGL; b++) {
+        const int e = emin + k0 + b;  // e <= 52 for the entries written; the others are computed and dropped
+        const double sc = __longlong_as_double((long long)(1023 + 52 - (e < 52 ? e : 52)) << 52);  // 2^(52 - e)
+        const double q = v * sc;
+        const double F = floor(q);
+        if (q - F == 0.5) {
+          const long long Fi = (long long)F;
+          d0[b] += (double)(Fi + ((p0[b] + Fi) & 1)); p0[b] = 0;
+          d1[b] += (double)(Fi + ((p1[b] + Fi) & 1)); p1[b] = 0;
+        } else {
+          const double R = rint(q);
+          const int Rp = (int)((long long)R & 1);
+          d0[b] += R; p0[b] = (p0[b] + Rp) & 1;
+          d1[b] += R; p1[b] = (p1[b] + Rp) & 1;
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < CT_BGL; b++) {
+      const int k = k0 + b;
+      if (k >= ne) continue;  // uniform
+      double2 v = ok ? make_double2(d0[b], d1[b] - d0[b]) : make_double2(nan, nan);
+      if (c < nstride) tab[(size_t)k * nstride + c] = v;
+      for (int l = 0; l < nlev; l++) {
+        const int st = 1 << l, L = l + 1;
+        const double2 r = make_double2(__shfl_down(v.x, st, 64), __shfl_down(v.y, st, 64));
+        if ((lane & (2 * st - 1)) == 0) {
+          v = compose_maps(v, r);
+          const int bb = c >> L;
+          if (bb < T.nb[L]) tree[T.off[L] + (size_t)k * T.nb[L] + bb] = v;
+        }
+      }
+    }
+  }
+}
+
 // levels L0 .. L0 + nlev - 1 of the block maps, nlev <= CT_SPAN: each wave takes 64 consecutive
 // entries of level L0 - 1 (level 0: the chunk table) of one binade, one per lane, and composes them
 // level by level across its lanes (lane i holds the block starting at entry i once i is a multiple
@@ -2838,10 +2909,6 @@ static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne, long long W) {
     HIPCHK(hipMalloc((void**)&S.d_ctab, sizeof(double2) * need), "hipMalloc chunk table");
     S.ctab_cap = need;
   }
-  const long long nthr = (long long)nstride * ((ne + CT_BG - 1) / CT_BG);
-  hipLaunchKernelGGL(chunk_table_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, c->ustream, S.d_pr,
-                     c->d_null, c->n_snps, emin, ne, nstride, S.d_ctab);
-  HIPCHK(hipGetLastError(), "launch chunk_table_kernel");
   S.ctree = CTree{};
   S.ctree.lmax = lmax;
   if (lmax > 0) {
@@ -2859,15 +2926,30 @@ static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne, long long W) {
       S.ctree_cap = tot;
     }
     S.ctree.p = S.d_ctree;
-    for (int L0 = 1; L0 <= lmax; L0 += CT_SPAN) {  // levels L0 .. L0 + nlev - 1 per launch, from level L0 - 1
-      const int nlev = std::min(CT_SPAN, lmax - L0 + 1);
-      const int nprev = L0 == 1 ? nstride : S.ctree.nb[L0 - 1];
-      const int ngrp = (nprev + 255) / 256;  // four waves of 64 entries per workgroup
-      if (ngrp == 0) break;
-      hipLaunchKernelGGL(chunk_tree_kernel, dim3((unsigned)(ne * ngrp)), dim3(256), 0, c->ustream, S.d_ctab, nstride,
-                         S.ctree, S.d_ctree, L0, nlev, ngrp);
-      HIPCHK(hipGetLastError(), "launch chunk_tree_kernel");
-    }
+  }
+  // FSCLG_CT_LDS=0: the table without LDS staging (one lane per chunk reading its sites), and every
+  // tree level by chunk_tree_kernel
+  static const int ct_lds = getenv("FSCLG_CT_LDS") ? atoi(getenv("FSCLG_CT_LDS")) : 1;
+  int L1 = 1;  // the first tree level chunk_tree_kernel builds
+  if (ct_lds) {
+    const int nlev = std::min(CT_SPAN, lmax);
+    hipLaunchKernelGGL(chunk_table_lds_kernel, dim3((unsigned)((nstride + 63) / 64)), dim3(256), 0, c->ustream,
+                       S.d_pr, c->d_null, c->n_snps, emin, ne, nstride, S.d_ctab, S.ctree, S.d_ctree, nlev);
+    L1 = nlev + 1;
+  } else {
+    const long long nthr = (long long)nstride * ((ne + CT_BG - 1) / CT_BG);
+    hipLaunchKernelGGL(chunk_table_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, c->ustream, S.d_pr,
+                       c->d_null, c->n_snps, emin, ne, nstride, S.d_ctab);
+  }
+  HIPCHK(hipGetLastError(), "launch chunk_table_kernel");
+  for (int L0 = L1; L0 <= lmax; L0 += CT_SPAN) {  // levels L0 .. L0 + nlev - 1 per launch, from level L0 - 1
+    const int nlev = std::min(CT_SPAN, lmax - L0 + 1);
+    const int nprev = L0 == 1 ? nstride : S.ctree.nb[L0 - 1];
+    const int ngrp = (nprev + 255) / 256;  // four waves of 64 entries per workgroup
+    if (ngrp == 0) break;
+    hipLaunchKernelGGL(chunk_tree_kernel, dim3((unsigned)(ne * ngrp)), dim3(256), 0, c->ustream, S.d_ctab, nstride,
+                       S.ctree, S.d_ctree, L0, nlev, ngrp);
+    HIPCHK(hipGetLastError(), "launch chunk_tree_kernel");
   }
   S.ctab_valid = true; S.ctab_emin = emin; S.ctab_ne = ne;
   return FSCLG_OK;
@@ -3456,6 +3538,19 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
     B.upos[u] = k;
   }
   if (use_ep) memcpy(B.p_epos, B.epos.data(), sizeof(int2) * ne);
+  if (G > 1) {  // the split cells' arrival counters, zeroed before the wait for the slot's rows (the
+                // fill then runs while the upload stream still works, off the blocking batch's path)
+    const size_t xb = (size_t)nl * 2 * sizeof(XAcc);
+    if (B.xacc_cap < xb) {
+      if (B.d_xacc) hipFree(B.d_xacc);
+      B.d_xacc = nullptr; B.xacc_cap = 0;
+      HIPCHK(hipMalloc((void**)&B.d_xacc, xb), "hipMalloc split accumulators");
+      B.xacc_cap = xb;
+    }
+    if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, nl))) return r;
+    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");  // the exchange
+                                                                                                  // areas need no zeroing
+  }
   // the slot's rows and null sums first
   HIPCHK(hipStreamWaitEvent(B.stream, c->slot[slot].ready, 0), "hipStreamWaitEvent");
   Params P = make_params(c, B, slot, nl, 0, eval_range, bp_resl);
@@ -3477,16 +3572,6 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
     c->n_ep_saved += (unsigned long long)(2 * nu - ne);
   }
   if (G > 1) {
-    const size_t xb = (size_t)nl * 2 * sizeof(XAcc);
-    if (B.xacc_cap < xb) {
-      if (B.d_xacc) hipFree(B.d_xacc);
-      B.d_xacc = nullptr; B.xacc_cap = 0;
-      HIPCHK(hipMalloc((void**)&B.d_xacc, xb), "hipMalloc split accumulators");
-      B.xacc_cap = xb;
-    }
-    if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, nl))) return r;
-    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");  // the exchange
-                                                                                                  // areas need no zeroing
     P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
     P.spec_refine = spec_refine_on();
     // latency: no LDS coefficient windows (their loads, repeated by every member for every

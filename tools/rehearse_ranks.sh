@@ -23,7 +23,11 @@ echo "usable CPUs: $U, W=$W"
 if [ "${WARM:-1}" = 1 ]; then  # warm caches (to a file: a long silent step looks hung to gpurun); WARM=0 skips it (C5)
   timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/warm.log 2>&1
 fi
-FSCL_AMD_SIM=record:$REC timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w1_record.json 2> $OUT/w1_record.err || exit 1
+if [ "${REUSE:-0}" = 1 ] && [ -s $REC ]; then  # REUSE=1: replay the recording an earlier call of this tag left
+  echo "reusing $REC"
+else
+  FSCL_AMD_SIM=record:$REC timeout -k 10 900 python3 -u $R/bench.py --config $CFG --warmup 0 --steps 1 --no-cpu-baseline > $OUT/w1_record.json 2> $OUT/w1_record.err || exit 1
+fi
 burn() {  # $1 spinning processes (BURN=yield: spinning with sched_yield, as the ranks' exchange waits do
           # after 4096 spins), each time-limited; their pids in BURN_PIDS
   BURN_PIDS=""
