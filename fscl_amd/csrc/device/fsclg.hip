@@ -3434,7 +3434,12 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
     // rehearsal 59.7 -> 47.3 s per job, profiles/r05d_c5_ranks); batches of more than 256 cells (every
     // one-GPU job's blocking batches but C5 chr1's) stay unsplit as before
     static const int budget = getenv("FSCLG_SPLIT_BUDGET") ? atoi(getenv("FSCLG_SPLIT_BUDGET")) : 512;
-    G = std::min(std::min(B.split_max, MAXSPLIT), budget / std::max(nu, 1));
+    // batches 2.. (the permutation pipeline's bulk batches, which run beside a blocking batch that
+    // may take the whole budget): a quarter of it, so that only a bulk batch of a few dozen cells
+    // is split (the pruned tail at 8 GPUs, a one-chromosome job) and one beside a large unsplit
+    // blocking batch (C4's one-GPU tail: 177 bulk cells beside 301) is not
+    static const int bulk_budget = getenv("FSCLG_BULK_BUDGET") ? atoi(getenv("FSCLG_BULK_BUDGET")) : 128;
+    G = std::min(std::min(B.split_max, MAXSPLIT), (batch >= 2 ? bulk_budget : budget) / std::max(nu, 1));
     if (G < 2) G = 1;
   }
   B.split = G;

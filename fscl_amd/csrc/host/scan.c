@@ -1420,6 +1420,15 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
                               int large_grid_sp, double scan_width_mb, fh_rand_t *g, int save) {
   const char *env = getenv("FSCL_AMD_DEPTH");
   const int K = env ? (atoi(env) < 2 ? 2 : (atoi(env) > FSCLG_N_SLOTS ? FSCLG_N_SLOTS : atoi(env))) : 4;
+  /* row slots (and bulk batches): S >= K trials' rows on the devices (FSCL_AMD_SLOTS, at most FSCLG_N_SLOTS).
+     The blocking class keeps the margin K; a bulk batch is waited only when its slot comes round, S
+     trials later, and a point that may draw before its bulk results are in drains them first. */
+  const char *senv = getenv("FSCL_AMD_SLOTS");
+  const int S = senv ? (atoi(senv) < K ? K : (atoi(senv) > FSCLG_N_SLOTS ? FSCLG_N_SLOTS : atoi(senv))) : K;
+  /* the bulk batches' cells get up to FSCL_AMD_BULK_SPLIT workgroups each when they are few (the
+     pruned tail), so that a bulk batch is done before its slot comes round again */
+  const char *bsenv = getenv("FSCL_AMD_BULK_SPLIT");
+  const int bulk_split = bsenv ? (atoi(bsenv) < 1 ? 1 : atoi(bsenv)) : 4;
   const int no_merge = getenv("FSCL_AMD_NO_MERGE") != NULL;  /* read once: every rank must decide alike */
   int *act, n_act = s->n_scan_pts, i, k, trial = -1, done = -1;
   pqueue_t *pq;
@@ -1428,12 +1437,17 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   memset(&A, 0, sizeof A);
   memset(Bt, 0, sizeof Bt);
   A.batch = 0; /* high-priority stream */
-  for (k = 0; k < K; k++) { Bt[k].batch = 2 + k; nul[k] = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums"); }
+  for (k = 0; k < S; k++) {
+    int l;
+    Bt[k].batch = 2 + k;
+    nul[k] = fh_malloc(sizeof(double) * (D.n_chr ? D.n_chr : 1), "null sums");
+    for (l = 0; l < D.n_dev; l++) dev_check(fsclg_set_batch_split(D.ctx[l], Bt[k].batch, bulk_split), "batch split");
+  }
   act = fh_malloc(sizeof(int) * (n_act ? n_act : 1), "active points");
   pq = fh_calloc(n_act ? n_act : 1, sizeof(pqueue_t), "result queues");
   if (D.world * D.n_dev > 1) g_pcost = fh_calloc(n_act ? n_act : 1, sizeof(double), "point costs");
   tb_reserve(&A, n_act ? n_act : 1);
-  for (k = 0; k < K; k++) tb_reserve(&Bt[k], n_act ? n_act : 1);
+  for (k = 0; k < S; k++) tb_reserve(&Bt[k], n_act ? n_act : 1);
   for (i = 0; i < n_act; i++) act[i] = i;
   FILE *tt = getenv("FSCL_AMD_TRIAL_TRACE") ? fopen(getenv("FSCL_AMD_TRIAL_TRACE"), "w") : NULL;  /* development aid */
   double tr[8];
@@ -1453,17 +1467,17 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   D.st.plan_mode = PM.on;
   /* the switches every rank's batches and collectives follow must agree (an environment variable
      set on one rank only would otherwise diverge the exchanges) */
-  ranks_agree("FSCL_AMD_DEPTH / FSCL_AMD_NO_MERGE / FSCL_AMD_PERM_LEADER / FSCL_AMD_PLAN*",
-              (uint64_t)K | (uint64_t)no_merge << 8 | (uint64_t)PL.on << 9 | (uint64_t)PM.on << 10 |
+  ranks_agree("FSCL_AMD_DEPTH / FSCL_AMD_SLOTS / FSCL_AMD_NO_MERGE / FSCL_AMD_PERM_LEADER / FSCL_AMD_PLAN*",
+              (uint64_t)K | (uint64_t)S << 4 | (uint64_t)no_merge << 8 | (uint64_t)PL.on << 9 | (uint64_t)PM.on << 10 |
               (uint64_t)(PM.on ? PM.ecap : 0) << 11 | (uint64_t)(PM.on ? PM.gcap : 0) << 40);
   spec_start();
   D.st.spec_threads = SP.n_th;
-  if (PL.on) pool_setup(s->n_snps, K);
-  else pb_reserve(s->n_snps, K);
+  if (PL.on) pool_setup(s->n_snps, S);
+  else pb_reserve(s->n_snps, S);
   D.st.perm_leader = PL.on;
   SP.snps = s->snps; SP.n = s->n_snps; SP.nbp = permute_nbp; SP.width_mb = scan_width_mb;
   for (;;) {
-    const int slot = (trial + 1) % K;
+    const int slot = (trial + 1) % S;
     trial_batch_t *B = &Bt[slot];
     double tp = fh_now();
     void *prow;
@@ -1629,7 +1643,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
         D.st.n_drain++;
         for (;;) {
           trial_batch_t *old = NULL;
-          for (k = 0; k < K; k++)
+          for (k = 0; k < S; k++)
             if (Bt[k].submitted && Bt[k].trial < trial && (!old || Bt[k].trial < old->trial)) old = &Bt[k];
           if (!old) break;
           tb_wait(old, pq);
@@ -1652,7 +1666,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
          (no draws among them) */
       for (;;) {
         trial_batch_t *old = NULL;
-        for (k = 0; k < K; k++)
+        for (k = 0; k < S; k++)
           if (Bt[k].submitted && (!old || Bt[k].trial < old->trial)) old = &Bt[k];
         if (!old) break;
         tb_wait(old, pq);
@@ -1665,7 +1679,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   for (;;) {
     trial_batch_t *old = NULL;
     double tp = fh_now();
-    for (k = 0; k < K; k++)
+    for (k = 0; k < S; k++)
       if (Bt[k].submitted && (!old || Bt[k].trial < old->trial)) old = &Bt[k];
     if (!old) break;
     tb_wait(old, pq);
@@ -1674,7 +1688,7 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   }
   for (i = 0; i < s->n_scan_pts; i++)
     if (pq[i].n) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline: unapplied results");
-  for (k = 0; k < K; k++) slot_release(k);  /* every upload has read its buffer */
+  for (k = 0; k < S; k++) slot_release(k);  /* every upload has read its buffer */
   spec_quiesce();
   PL.on = 0;
   PL.sizing = 0;
@@ -1682,7 +1696,12 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   g_null_nt = 0;
   if (tt) fclose(tt);
   tb_free(&A);
-  for (k = 0; k < K; k++) { tb_free(&Bt[k]); free(nul[k]); }
+  for (k = 0; k < S; k++) {
+    int l;
+    for (l = 0; l < D.n_dev; l++) dev_check(fsclg_set_batch_split(D.ctx[l], Bt[k].batch, 1), "batch split");
+    tb_free(&Bt[k]);
+    free(nul[k]);
+  }
   free(act); free(pq);
   free(g_pcost); g_pcost = NULL;
 }

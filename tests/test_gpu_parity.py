@@ -414,6 +414,19 @@ def test_pipelined_trials_match_lockstep_and_oracle(built, tmp, monkeypatch):
     monkeypatch.setenv("FSCL_AMD_LOCKSTEP", "1")
     scan = fscl_amd.run(snp, tmp / "l.txt", **_kw(opts))
     assert (tmp / "l.txt").read_text() == (tmp / "o.txt").read_text()
+    monkeypatch.delenv("FSCL_AMD_LOCKSTEP")
+    # other pipeline shapes: more row slots than the blocking margin (a bulk batch waited only
+    # when its slot comes round, S trials later; a point that may draw first drains them), bulk
+    # batches split over several workgroups per cell, and both with a margin of 2
+    for env in ({"FSCL_AMD_SLOTS": "8"}, {"FSCL_AMD_BULK_SPLIT": "4"}, {"FSCL_AMD_BULK_SPLIT": "1"},
+                {"FSCL_AMD_DEPTH": "2", "FSCL_AMD_SLOTS": "8", "FSCL_AMD_BULK_SPLIT": "8"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        scan = fscl_amd.run(snp, tmp / "s.txt", **_kw(opts))
+        assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(tmp / "o.dump"), f"pipelined {env}")
+        assert (tmp / "s.txt").read_text() == (tmp / "o.txt").read_text(), env
+        for k in env:
+            monkeypatch.delenv(k)
 
 
 def test_c2_scale_scan_and_short_permutation(built, tmp):
