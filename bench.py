@@ -525,7 +525,7 @@ def bench_line(args, cfg: dict, st: dict, units: float, elapsed: float, n_gpus: 
                                      "n_ep_saved", "wait_s", "n_crit", "n_drain", "spec_threads", "spec_posted",
                                      "spec_hits", "spec_cands", "spec_wait_s", "spec_done", "spec_gen_s",
                                      "spec_claimed", "n_merged", "perm_leader", "plan_mode", "plan_fallback",
-                                     "spec_rank", "n_split_retry")},
+                                     "spec_rank", "n_split_retry", "prestaged", "prestage_hits")},
     }
 
 

@@ -86,7 +86,7 @@ class Stats(C.Structure):  # fscl_amd_stats_t
                 ("spec_done", C.c_ulonglong), ("spec_gen_s", C.c_double),
                 ("n_split_retry", C.c_ulonglong), ("spec_claimed", C.c_ulonglong), ("n_merged", C.c_ulonglong),
                 ("perm_leader", C.c_int), ("plan_mode", C.c_int), ("plan_fallback", C.c_ulonglong),
-                ("spec_rank", C.c_ulonglong * 8)]
+                ("spec_rank", C.c_ulonglong * 8), ("prestaged", C.c_ulonglong), ("prestage_hits", C.c_ulonglong)]
 
     def as_dict(self) -> dict:
         return {k: (list(v) if isinstance(v, C.Array) else v) for k, v in ((k, getattr(self, k)) for k, _ in self._fields_)}

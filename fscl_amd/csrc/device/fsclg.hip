@@ -2678,6 +2678,25 @@ int fsclg_slot_wait(fsclg_ctx* c, int slot) {
   return FSCLG_OK;
 }
 
+int fsclg_slot_swap(fsclg_ctx* c, int a, int b) {
+  if (!c) return set_err(FSCLG_E_ARG, "ctx");
+  if (a < 0 || a >= NSLOT || b < 0 || b >= NSLOT) return set_err(FSCLG_E_ARG, "slot");
+  if (c->slot[a].users || c->slot[b].users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
+  if (a != b) std::swap(c->slot[a], c->slot[b]);
+  return FSCLG_OK;
+}
+
+int fsclg_search_done(fsclg_ctx* c, int batch) {
+  if (!c || batch < 0 || batch >= NBATCH) return set_err(FSCLG_E_ARG, "batch");
+  Batch& B = c->batch[batch];
+  if (!B.pending || B.n_cells == 0) return 1;
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  const hipError_t q = hipEventQuery(B.ev2);
+  if (q == hipErrorNotReady) return 0;
+  HIPCHK(q, "hipEventQuery");
+  return 1;
+}
+
 int fsclg_slot_set_rows_host(fsclg_ctx* c, int slot, const uint32_t* row, const double* chr_null) {
   return fsclg_slot_set_rows_packed(c, slot, row, 4, chr_null);
 }
@@ -3144,6 +3163,9 @@ static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, 
   Slot& S = c->slot[slot];
   if (S.users) return set_err(FSCLG_E_STATE, "slot in use by a batch not waited for");
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  // the slot's rows unchanged since its sums were made (a trial prepared ahead in a spare slot for
+  // a superset of these cells, fsclg_slot_swap): only what is missing
+  if (S.win_valid && S.win_er == eval_range) return ensure_windows(c, slot, eval_range, cells, n_cells, &c->wr_memo);
   const long long W = 2ll * eval_range + 1;
   // cost in waves with windows to sum (a wave: 64 threads x WN_PER windows; a block's waves
   // without windows only stage tiles)

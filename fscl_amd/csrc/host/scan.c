@@ -835,6 +835,7 @@ static void sigint_dump(scan_t *s, int n_perm) {
 #define PB_FREE (-1)
 #define PB_CAND (-2)
 #define PB_HELD (-3)
+#define PB_PRE (-4)   /* a candidate a spare device slot is being prepared from (pre-staging) */
 
 typedef struct {
   void *buf;       /* one trial's rows (D.rb bytes each), pinned: every local device's upload reads it */
@@ -1476,12 +1477,27 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   else pb_reserve(s->n_snps, S);
   D.st.perm_leader = PL.on;
   SP.snps = s->snps; SP.n = s->n_snps; SP.nbp = permute_nbp; SP.width_mb = scan_width_mb;
+  /* pre-staging (plan mode, one process of one rank): while trial t's blocking batch runs, the
+     likeliest candidate for trial t + 1 -- once a worker has built it -- is applied to a spare
+     device slot with its window sums; when it is the one taken, the slot is swapped in and the
+     trial's upload chain (plan kernels, window sums) is off its critical path.  FSCL_AMD_PRESTAGE=0:
+     off.  Not with several ranks (the leader's candidates are not the other ranks'). */
+  const char *pse = getenv("FSCL_AMD_PRESTAGE");
+  /* FSCL_AMD_PRESTAGE=n: the n likeliest candidates, in spare slots S .. S + n - 1 */
+  int n_pre = pse ? atoi(pse) : 2;  /* 2: C5 one chromosome 15.1 s against 15.4 s with 1, 15.3 s with 3 */
+  if (n_pre > FSCLG_N_SLOTS - S) n_pre = FSCLG_N_SLOTS - S;
+  if (!(PM.on && D.world == 1 && !PL.on && SP.n_th > 0)) n_pre = 0;
+  if (n_pre < 0) n_pre = 0;
+  const int pre_on = n_pre > 0;
+  int pre_bi[FSCLG_N_SLOTS];  /* the candidate buffer spare slot S + i was prepared from (owner PB_PRE), or -1 */
+  for (k = 0; k < FSCLG_N_SLOTS; k++) pre_bi[k] = -1;
   for (;;) {
     const int slot = (trial + 1) % S;
     trial_batch_t *B = &Bt[slot];
     double tp = fh_now();
     void *prow;
     int rows_here = 0;  /* plan mode: this trial's rows were built on the host into D.stage[slot] */
+    int use_pre = 0;    /* this trial's permutation was pre-staged in spare slot use_pre (>= S), swapped in */
     tr[0] = tp;
     /* the slot's previous trial: its bulk results (no draws among them) */
     if (B->submitted) {
@@ -1515,6 +1531,16 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       /* this trial's permutation: the candidate for the previous trial's draw count, else built here */
       bi = posted ? spec_take((int)(g_draws - draw_mark), g) : -1;
       from_spec = bi >= 0;
+      for (k = 0; k < n_pre; k++) {
+        if (pre_bi[k] < 0) continue;
+        if (bi == pre_bi[k]) use_pre = S + k;  /* this spare slot holds the trial */
+        else {  /* not taken: free its buffer once the spare's upload has read it */
+          int l;
+          for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_wait(D.ctx[l], S + k), "slot wait");
+          if (SP.pb[pre_bi[k]].owner == PB_PRE) SP.pb[pre_bi[k]].owner = PB_FREE;
+        }
+        pre_bi[k] = -1;
+      }
       if (bi < 0) {
         bi = pb_get();
         if (PM.on) {
@@ -1560,7 +1586,11 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
     memcpy(nul[slot], pnul, sizeof(double) * (D.n_chr ? D.n_chr : 1));
     tp = fh_now();
     if (rows_here) slot_upload_buf(slot, D.stage[slot], nul[slot]);
-    else {
+    else if (use_pre) {
+      int l;
+      for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_swap(D.ctx[l], slot, use_pre), "slot swap");
+      D.st.prestage_hits++;
+    } else {
       if (PL.on && !PL.registered) {  /* the pool is not page-locked here: through the slot's own staging */
         memcpy(D.stage[slot], prow, PM.on ? PM.bytes : (size_t)D.rb * (size_t)s->n_snps);
         prow = D.stage[slot];
@@ -1622,6 +1652,26 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
       spec_post(g, dl, spec_candidates(s, pq, &A, spec_ncand(), dl));
     }
     draw_mark = g_draws;
+    for (k = 0; pre_on && posted && A.n > 0 && k < n_pre; k++) {
+      /* the k-th likeliest candidate, if a worker finishes it before the blocking batch is done */
+      int st0 = 0, b0 = -1, done = 0;
+      for (;;) {
+        int l;
+        pthread_mutex_lock(&SP.mu);
+        if (SP.n_job > k) { st0 = SP.state[k]; b0 = SP.bi[k]; } else st0 = 3;
+        if (st0 == 2) SP.pb[b0].owner = PB_PRE;  /* spec_take's cancelling leaves it alone */
+        pthread_mutex_unlock(&SP.mu);
+        if (st0 >= 2) break;
+        for (done = 1, l = 0; l < D.n_dev && done; l++) done = fsclg_search_done(D.ctx[l], A.batch) > 0;
+        if (done) break;
+        sched_yield();
+      }
+      if (st0 != 2) break;
+      slot_upload_plan(S + k, SP.pb[b0].buf, SP.pb[b0].nul);
+      trial_windows(S + k, &A, B, eval_range);
+      pre_bi[k] = b0;
+      D.st.prestaged++;
+    }
     {
       int drain = 0, m = 0;
       for (k = 0; k < A.n; k++) m += s->scan_pts[A.pt[k]].permute_p + pq[A.pt[k]].n >= 20;
@@ -1688,6 +1738,12 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   }
   for (i = 0; i < s->n_scan_pts; i++)
     if (pq[i].n) logmsg(MSG_FATAL, "fscl_amd: permutation pipeline: unapplied results");
+  for (k = 0; k < n_pre; k++) {  /* the spare slots' last uploads have read their buffers (a trial that did
+                                    not come, or one taken just before the last trial ended the loop) */
+    int l;
+    for (l = 0; l < D.n_dev; l++) dev_check(fsclg_slot_wait(D.ctx[l], S + k), "slot wait");
+    if (pre_bi[k] >= 0 && SP.pb[pre_bi[k]].owner == PB_PRE) SP.pb[pre_bi[k]].owner = PB_FREE;
+  }
   for (k = 0; k < S; k++) slot_release(k);  /* every upload has read its buffer */
   spec_quiesce();
   PL.on = 0;

@@ -240,6 +240,9 @@ typedef struct {
   unsigned long long plan_fallback; /* plan mode: trials whose plan did not fit its buffer (rows instead) */
   unsigned long long spec_rank[8];  /* speculation hits by the candidate's rank in the likeliest-first order
                                        (7: rank 7 or later): how many launched-ahead candidates would cover */
+  unsigned long long prestaged;     /* plan mode, one process: trials whose likeliest candidate was applied to a
+                                       spare device slot (with its window sums) while the trial before ran */
+  unsigned long long prestage_hits; /*   of which it was the trial's permutation (its upload skipped) */
 } fscl_amd_stats_t;
 void fscl_amd_get_stats(fscl_amd_stats_t *st);
 void fscl_amd_reset_stats(void);

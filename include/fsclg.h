@@ -149,6 +149,12 @@ void fsclg_host_free(void *p);
 int fsclg_host_register(void *p, size_t bytes);
 int fsclg_host_unregister(void *p);
 int fsclg_slot_wait(fsclg_ctx *c, int slot);
+/* exchange two slots' device state (rows, window sums, their upload events): a trial prepared in
+   a spare slot ahead of time becomes slot a.  Neither slot may have a batch not waited for. */
+int fsclg_slot_swap(fsclg_ctx *c, int a, int b);
+/* 1 if the batch's last submit has completed (or none is pending), 0 if it is still running:
+   fsclg_search_wait would not block */
+int fsclg_search_done(fsclg_ctx *c, int batch);
 int fsclg_slot_set_rows_host(fsclg_ctx *c, int slot, const uint32_t *row, const double *chr_null);
 /* the same with rows of row_bytes = 1, 2 or 4 bytes each (1: n_rows <= 256, 2: n_rows <= 65536):
    a narrower staging is fewer PCIe bytes for every device's upload of every trial */

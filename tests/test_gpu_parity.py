@@ -327,17 +327,21 @@ def _windowed_genome(tmp, seed=93):
     return snp, ["--coarse-grid-spacing=100000", "--n-permute=60", "--eval-range=300"]
 
 
-@pytest.mark.parametrize("variant", ["plan", "rows", "fallback"])
+@pytest.mark.parametrize("variant", ["plan", "plan_no_prestage", "rows", "fallback"])
 def test_block_plan_on_the_device_matches_oracle(built, tmp, monkeypatch, variant):
     """Each trial's block permutation as a plan the device applies (fsclg_slot_set_rows_plan,
-    DESIGN.md §5.6): the default where no whole-chromosome null sum is read; FSCL_AMD_PLAN=0 the
-    rows built on the host; FSCL_AMD_PLAN_ECAP=1 plan buffers too small for any plan, so every
-    trial falls back to host rows.  60 permutations with pruning: bit-identical to the oracle."""
+    DESIGN.md §5.4): the default where no whole-chromosome null sum is read, with the likeliest
+    next candidate applied to a spare slot ahead (pre-staging, swapped in when taken), or without
+    (FSCL_AMD_PRESTAGE=0); FSCL_AMD_PLAN=0 the rows built on the host; FSCL_AMD_PLAN_ECAP=1 plan
+    buffers too small for any plan, so every trial falls back to host rows.  60 permutations with
+    pruning: bit-identical to the oracle."""
     snp, opts = _windowed_genome(tmp)
     if variant == "rows":
         monkeypatch.setenv("FSCL_AMD_PLAN", "0")
     if variant == "fallback":
         monkeypatch.setenv("FSCL_AMD_PLAN_ECAP", "1")
+    if variant == "plan_no_prestage":
+        monkeypatch.setenv("FSCL_AMD_PRESTAGE", "0")
     run_oracle(snp, tmp / "o.txt", opts, tmp / "o.dump")
     fscl_amd.reset_stats()
     scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(opts))
@@ -348,6 +352,10 @@ def test_block_plan_on_the_device_matches_oracle(built, tmp, monkeypatch, varian
     assert (tmp / "g.txt").read_text() == (tmp / "o.txt").read_text()
     assert st["plan_mode"] == (variant != "rows")
     assert (st["plan_fallback"] > 0) == (variant == "fallback")
+    if variant == "plan":  # spare slots were prepared and some were taken
+        assert st["prestage_hits"] > 0 and st["prestaged"] >= st["prestage_hits"], st
+    if variant in ("plan_no_prestage", "rows"):
+        assert st["prestaged"] == 0
 
 
 @pytest.mark.parametrize("variant", ["pool", "pool_copy", "pool_fallback"])
