@@ -1948,7 +1948,7 @@ __global__ void __launch_bounds__(256) chunk_tree_kernel(const double2* __restri
 __global__ void __launch_bounds__(WN_WG)
 window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nullrow,
                     const int2* __restrict__ tasks, int W, int emin, int ne, int nstride,
-                    const double2* __restrict__ tab, double* __restrict__ out, CTree T) {
+                    const double2* __restrict__ tab, double* __restrict__ out, CTree T, int wdesc) {
   __builtin_amdgcn_s_setprio(2);  // beside the search kernels' waves, which wait on memory
   const int2 t = tasks[blockIdx.x];
   const int lane = threadIdx.x & 63;
@@ -1977,16 +1977,41 @@ window_chunk_kernel(const uint2* __restrict__ pr, const double* __restrict__ nul
         const double isc = __longlong_as_double((long long)(1023 - 52 + eu) << 52);  // 2^(e - 52)
         double m = s * sc;
         int L = T.lmax;
+        auto entry = [&](int cc, int l) -> cdouble* {  // block (cc, level l) of binade eu
+          return l == 0 ? (cdouble*)(tab + (size_t)(eu - emin) * nstride + cc)
+                        : (cdouble*)(T.p + T.off[l] + (size_t)(eu - emin) * T.nb[l] + (cc >> l));
+        };
+        auto step = [&](double d0, double dd) {  // m after the block, if no lane leaves the binade
+          return m + __builtin_fma((double)(__double2loint(m) & 1), dd, d0);
+        };
         while (c < fast_hi) {  // uniform
           int Lc = min(L, 31 - __clz(fast_hi - c));
           if (c) Lc = min(Lc, __ffs(c) - 1);
-          cdouble* tb = Lc == 0 ? (cdouble*)(tab + (size_t)(eu - emin) * nstride + c)
-                                : (cdouble*)(T.p + T.off[Lc] + (size_t)(eu - emin) * T.nb[Lc] + (c >> Lc));
+          cdouble* tb = entry(c, Lc);
           const double d0 = tb[0], dd = tb[1];
-          const double mn = m + __builtin_fma((double)(__double2loint(m) & 1), dd, d0);
-          if (__builtin_amdgcn_ballot_w64(!(mn > -TWO53)) == 0ull) { m = mn; c += 1 << Lc; L = T.lmax; }
-          else if (Lc == 0) break;
-          else L = Lc - 1;
+          const double mn = step(d0, dd);
+          if (__builtin_amdgcn_ballot_w64(!(mn > -TWO53)) == 0ull) { m = mn; c += 1 << Lc; L = T.lmax; continue; }
+          if (Lc == 0) break;
+          if (!wdesc || Lc < 2) { L = Lc - 1; continue; }
+          // a crossing inside [c, c + 2^Lc): the next two levels of the halving search from one
+          // round trip -- (c, Lc - 1), then (c + 2^(Lc-1), Lc - 2) after a success or (c, Lc - 2)
+          // after a failure, the same blocks in the same order as one level at a time
+          const int l1 = Lc - 1, l2 = Lc - 2;
+          cdouble* ta = entry(c, l1);
+          cdouble* tbs = entry(c + (1 << l1), l2);
+          cdouble* tcf = entry(c, l2);
+          const double a0 = ta[0], ad = ta[1], b0 = tbs[0], bd = tbs[1], f0 = tcf[0], fd = tcf[1];
+          const double ma = step(a0, ad);
+          if (__builtin_amdgcn_ballot_w64(!(ma > -TWO53)) == 0ull) {
+            m = ma; c += 1 << l1;
+            const double mb = step(b0, bd);
+            if (__builtin_amdgcn_ballot_w64(!(mb > -TWO53)) == 0ull) { m = mb; c += 1 << l2; L = T.lmax; continue; }
+          } else {
+            const double mf = step(f0, fd);
+            if (__builtin_amdgcn_ballot_w64(!(mf > -TWO53)) == 0ull) { m = mf; c += 1 << l2; L = T.lmax; continue; }
+          }
+          if (l2 == 0) break;
+          L = l2 - 1;
         }
         s = m * isc;
         if (c >= fast_hi) continue;
@@ -2103,13 +2128,35 @@ __global__ void __launch_bounds__(64) scatter_rows_kernel(uint2* __restrict__ pr
 // the upload stream, in stream order.
 __global__ void __launch_bounds__(256) plan_swap_kernel(uint2* __restrict__ pr, const fsclg_swap_t* __restrict__ ent,
                                                         int e0) {
+  // a thread's sites of both ranges are loaded three at a time before they are stored: one memory
+  // latency per 768 sites of the entry instead of one per 256 (the stores may alias the next loads
+  // as far as the compiler can tell, so a load-store loop waits for each round trip); three keep the
+  // kernel within the 32 registers the search waves leave free
+#ifndef FSCLG_SWAP_PER
+#define FSCLG_SWAP_PER 3
+#endif
+  constexpr int PER = FSCLG_SWAP_PER;
   const fsclg_swap_t x = ent[e0 + blockIdx.x];
-  for (int t = threadIdx.x; t < x.len; t += 256) {
-    uint32_t* a = &pr[phys((uint32_t)(x.i + t))].y;
-    uint32_t* b = &pr[phys((uint32_t)(x.j + t))].y;
-    const uint32_t va = *a, vb = *b;
-    *a = vb;
-    *b = va;
+  char* rw = reinterpret_cast<char*>(pr) + 4;  // the row words; 32-bit byte offsets (scalar base + vector offset)
+  auto row = [rw](uint32_t i) -> uint32_t& { return *reinterpret_cast<uint32_t*>(rw + (phys(i) << 3)); };
+  for (int t0 = threadIdx.x; t0 < x.len; t0 += 256 * PER) {
+    uint32_t va[PER], vb[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int t = t0 + 256 * k;
+      if (t < x.len) {
+        va[k] = row((uint32_t)(x.i + t));
+        vb[k] = row((uint32_t)(x.j + t));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int t = t0 + 256 * k;
+      if (t < x.len) {
+        row((uint32_t)(x.i + t)) = vb[k];
+        row((uint32_t)(x.j + t)) = va[k];
+      }
+    }
   }
 }
 
@@ -2913,6 +2960,12 @@ static bool chunk_params(fsclg_ctx* c, long long W, int& emin, int& ne) {
 // entries per binade of the chunk table: the chunks, then WCG padding entries for a group's reads
 static int ctab_stride(const fsclg_ctx* c) { return (c->n_snps + WC - 1) / WC + WCG; }
 
+// window_chunk_kernel's halving search two levels per round trip (FSCLG_WIN_DESC=0: one)
+static int win_desc() {
+  static const int d = getenv("FSCLG_WIN_DESC") ? atoi(getenv("FSCLG_WIN_DESC")) : 1;
+  return d;
+}
+
 // the slot's chunk table (after its rows' upload, on the upload stream)
 static int ensure_ctab(fsclg_ctx* c, Slot& S, int emin, int ne, long long W) {
   // block levels up to the window's length in chunks (FSCLG_WINDOW_TREE=0: none, one step per chunk)
@@ -3033,7 +3086,7 @@ static int ensure_windows(fsclg_ctx* c, int slot, int er, const fsclg_cell_t* ce
     if (chunked) {
       if ((r = ensure_ctab(c, S, emin, ne, W))) return r;
       hipLaunchKernelGGL(window_chunk_kernel, dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null,
-                         c->d_wtasks, (int)W, emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null, S.ctree);
+                         c->d_wtasks, (int)W, emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null, S.ctree, win_desc());
     } else {
       hipLaunchKernelGGL((window_null_kernel<WN_PER>), dim3(c->n_wtasks), dim3(WN_WG), 0, c->ustream, S.d_pr,
                          c->d_null, c->d_wtasks, (int)W, S.d_win_null);
@@ -3125,7 +3178,7 @@ static int launch_partial_windows(fsclg_ctx* c, Slot& S, int er, const std::vect
   if (chunk_mode >= 1 && chunk_params(c, 2ll * er + 1, emin, ne)) {
     if ((r = ensure_ctab(c, S, emin, ne, 2ll * er + 1))) return r;
     hipLaunchKernelGGL(window_chunk_kernel, dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
-                       (int)(2ll * er + 1), emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null, S.ctree);
+                       (int)(2ll * er + 1), emin, ne, ctab_stride(c), S.d_ctab, S.d_win_null, S.ctree, win_desc());
   } else {
     hipLaunchKernelGGL((window_null_kernel<1>), dim3(nt), dim3(WN_WG), 0, c->ustream, S.d_pr, c->d_null, S.p_wtasks,
                        (int)(2ll * er + 1), S.d_win_null);
