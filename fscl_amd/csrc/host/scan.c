@@ -1477,13 +1477,13 @@ static void permute_pipelined(scan_t *s, int n_perm, double permute_nbp, int eva
   else pb_reserve(s->n_snps, S);
   D.st.perm_leader = PL.on;
   SP.snps = s->snps; SP.n = s->n_snps; SP.nbp = permute_nbp; SP.width_mb = scan_width_mb;
-  /* pre-staging (plan mode, one process of one rank): while trial t's blocking batch runs, the
-     likeliest candidate for trial t + 1 -- once a worker has built it -- is applied to a spare
-     device slot with its window sums; when it is the one taken, the slot is swapped in and the
-     trial's upload chain (plan kernels, window sums) is off its critical path.  FSCL_AMD_PRESTAGE=0:
-     off.  Not with several ranks (the leader's candidates are not the other ranks'). */
+  /* pre-staging (plan mode, one process of one rank): while trial t's blocking batch runs, each of
+     the likeliest candidates for trial t + 1 that a worker has finished by then is applied to a
+     spare device slot with its window sums; when one is taken, its slot is swapped in and the
+     trial's upload chain (plan kernels, window sums) is off its critical path.  Not with several
+     ranks (the leader's candidates are not the other ranks').  FSCL_AMD_PRESTAGE=n: the n
+     likeliest, in spare slots S .. S + n - 1 (0: off) */
   const char *pse = getenv("FSCL_AMD_PRESTAGE");
-  /* FSCL_AMD_PRESTAGE=n: the n likeliest candidates, in spare slots S .. S + n - 1 */
   int n_pre = pse ? atoi(pse) : 2;  /* 2: C5 one chromosome 15.1 s against 15.4 s with 1, 15.3 s with 3 */
   if (n_pre > FSCLG_N_SLOTS - S) n_pre = FSCLG_N_SLOTS - S;
   if (!(PM.on && D.world == 1 && !PL.on && SP.n_th > 0)) n_pre = 0;
