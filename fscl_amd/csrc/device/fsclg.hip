@@ -3508,7 +3508,10 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
     // 512 (round 5): at 8 GPUs C5's tail batches of ~69 cells get 7 members instead of 3 (the rank-0
     // rehearsal 59.7 -> 47.3 s per job, profiles/r05d_c5_ranks); batches of more than 256 cells (every
     // one-GPU job's blocking batches but C5 chr1's) stay unsplit as before
-    static const int budget = getenv("FSCLG_SPLIT_BUDGET") ? atoi(getenv("FSCLG_SPLIT_BUDGET")) : 512;
+    // 256 where the LDS coefficient window serves much of the terms (C2: 49 %, C3: 35 %), which split
+    // launches run without: there 512 cost C2 5 % and C3 9 % per job (HISTORY §R5.13)
+    static const int budget_env = getenv("FSCLG_SPLIT_BUDGET") ? atoi(getenv("FSCLG_SPLIT_BUDGET")) : 0;
+    const int budget = budget_env > 0 ? budget_env : (c->c_cover >= 0.3 ? 256 : 512);
     // batches 2.. (the permutation pipeline's bulk batches, which run beside a blocking batch that
     // may take the whole budget): a quarter of it, so that only a bulk batch of a few dozen cells
     // is split (the pruned tail at 8 GPUs, a one-chromosome job) and one beside a large unsplit
