@@ -392,6 +392,10 @@ def main() -> int:
         if fx is None and sfx is None:
             out["max_abs_dclr"] = scan_dclr
     if rank == 0:
+        live = (out.get("cpu_baseline") or {}).get("node_linear", {}).get("job_s")
+        out["north_star_ratio"] = north_star_ratio(args, n_permute, elapsed / args.steps, n_gpus, live)
+        if out.get("cpu_baseline"):
+            out["cpu_baseline"]["north_star_ratio"] = (out["north_star_ratio"] or {}).get("value")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -528,6 +532,34 @@ def bench_line(args, cfg: dict, st: dict, units: float, elapsed: float, n_gpus: 
                                      "spec_rank", "n_split_retry", "prestaged", "prestage_hits")},
     }
 
+
+
+NODE_LINEAR_TABLE = ROOT / "profiles" / "cpu_node_linear.json"
+NORTH_STAR_TARGET = 100.0  # BASELINE.json north_star: >= 100x the reference CPU's wall clock (C4 job, 8 GPUs)
+
+
+def north_star_ratio(args, n_permute: int, gpu_job_s: float, n_gpus: int, live_node_s: float | None = None):
+    """Where this line stands against the north star's >= 100x bar: the node-linear CPU job seconds of this
+    workload (the reference's compiled hot path over all the node's physical cores, perfectly scaled) over
+    this run's seconds per job.  The CPU figure is this run's own (cpu_baseline.node_linear) when it timed
+    the CPU, else the committed one of the same workload (profiles/cpu_node_linear.json); None without."""
+    src = "this run's cpu_baseline.node_linear"
+    node_s = live_node_s
+    if node_s is None:
+        key = f"{args.config}/chr{args.chromosomes or 'all'}/p{n_permute}/{args.permute_mode}"
+        try:
+            ent = json.loads(NODE_LINEAR_TABLE.read_text())["workloads"].get(key)
+        except (OSError, ValueError, KeyError):
+            ent = None
+        if not ent:
+            return None
+        node_s, src = float(ent["job_s"]), f"{NODE_LINEAR_TABLE.relative_to(ROOT)}[{key}] <- {ent['source']}"
+    ratio = node_s / gpu_job_s if gpu_job_s > 0 else None
+    return {"value": ratio, "n_gpus": n_gpus, "target": NORTH_STAR_TARGET,
+            "meets_target": bool(ratio is not None and ratio >= NORTH_STAR_TARGET),
+            "node_linear_job_s": node_s, "gpu_job_s": gpu_job_s, "source": src,
+            "what": "node-linear CPU seconds per job (reference code, one thread per cell, over the node's "
+                    "physical cores, plus the serial permutations) / this run's seconds per job"}
 
 
 def _harness(snp, cfg, threads, n_cells):

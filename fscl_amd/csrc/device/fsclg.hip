@@ -129,6 +129,10 @@ struct Params {
   const int32_t* n_refine;     // [n_coarse + 1]
   const uint32_t* dfail;       // [n_coarse + (n_coarse + 1) * MAXREF]: per alpha, the least |d| with
                                // logt(|d|) + lalpha > LOG_AD_MAX (logt is nondecreasing in |d|)
+  const uint32_t* dband;       // [alpha row][n_iv + 1]: the least |d| with logt(|d|) + lalpha >= thr[j] (band cuts)
+  int nd;                      // n_iv + 1 (dband's row stride)
+  int band_th;                 // a band's window is staged when its pieces hold at least this many trips
+  const int32_t* tpos;         // [ceil(n_snps / 128)]: the position of site 128 t (band cut searches)
   const fsclg_cell_t* cells;
   fsclg_point_t* out;
   unsigned long long* stats;   // 8 counters
@@ -196,12 +200,40 @@ struct Walk {
   double la;
   double xl, xr;  // log(alpha d) at the walk's far ends (the walk's largest x is one of them)
   uint32_t dfail; // a site is outside the walk iff its |d| >= dfail (Params::dfail)
-  int pad_;
+  int kd;         // the walk's alpha row in Params::dfail / Params::dband
 };
 
-template <int MW>
+// band mode (the throughput kernel): a phase's walks are evaluated interval band by
+// band.  Band b holds the intervals [bbase[b], bbase[b] + K) (K: the LDS window), the bands tile
+// downwards from the top interval of the phase's walks, and below the last one lies the remainder.
+// A walk part's sites in band b are those with |d| in [D(bbase[b]), D(bbase[b - 1])) (Params::dband):
+// one contiguous run of sites, a "piece", found as a trip range (cut[]: the trip holding the cut,
+// relative to the part's first trip; -1: the part never reaches the band) whose boundary trips
+// are masked by the same |d| test ("lazy cuts", run_piece_seg).  Pieces are cut into segments of
+// TPS trips; sb[] numbers a walk's segments in site-index order (left part's pieces from band 0 down
+// to the remainder, then the right part's from the remainder up to band 0).
+#ifndef FSCLG_NBMAX
+#define FSCLG_NBMAX 8
+#endif
+constexpr int NBMAX = FSCLG_NBMAX;
+constexpr int NPIECE = 2 * (NBMAX + 1);  // pieces per walk
+struct BandLds {
+  int16_t cut[MAXWALK][2][NBMAX];
+  uint8_t sb[MAXWALK][NPIECE + 1];
+  int bbase[NBMAX];
+  int nb;
+  int nrun;
+  int run_g0[NBMAX + 2];            // run r: groups (= bands, nb: the remainder) [run_g0[r], run_g0[r + 1])
+  int run_stage[NBMAX + 1];         // run r stages band run_g0[r]'s window first (0: keeps the loaded one)
+  int gitems[NBMAX + 1];            // segments per group
+  int gtrips[NBMAX + 1];            // trips per group
+};
+struct NoBand {};
+
+template <int MW, bool BAND = false>
 struct SmemT {
   static constexpr int MAXW = MW;
+  static constexpr bool HAS_BAND = BAND;
   Pt pt[4];                       // cells: start, end, midpoint, the midpoint's predicted child
   Walk w[MW];
   unsigned long long P[MW];
@@ -236,8 +268,9 @@ struct SmemT {
   int xfail;                      // split cells: PF_SPLIT_TIMEOUT if a member never arrived
   int iev;                        // FSCLG_INST_TRACE: events recorded so far
   int xnt[FSCLG_MAXSPLIT];        // split cells: each member's tie count of the instance
+  typename std::conditional<BAND, BandLds, NoBand>::type bd;
 };
-using Smem = SmemT<MAXWALK>;             // the throughput kernel (its LDS window takes the rest)
+using Smem = SmemT<MAXWALK, true>;       // the throughput kernel (its LDS window takes the rest)
 using SmemSplit = SmemT<MAXWALK_SPLIT>;  // split cells: room for speculative refine walks (no LDS window)
 
 
@@ -432,8 +465,13 @@ __device__ __forceinline__ void coef_stage(const double (&x)[U], const uint32_t 
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t ci = (uint32_t)(iv[u] - ivc0);
+#ifdef FSCLG_EXP_COEF_LDS  // timing ablation (wrong results): every coefficient from the LDS window
+      if (P.n_civ > 0)
+        coef_ld(fsclg_dyn, coef_off(rv[u], (int)min(ci, (uint32_t)P.civ_max), P), P, ca[u], cb[u]);
+#else
       if (ci < (uint32_t)P.n_civ)  // every row is cached
         coef_ld(fsclg_dyn, coef_off(rv[u], (int)ci, P), P, ca[u], cb[u]);
+#endif
       else
         coef_ld(reinterpret_cast<const char*>(P.coef), coef_off(rv[u], iv[u], P), P, ca[u], cb[u]);
     }
@@ -814,8 +852,13 @@ __device__ __forceinline__ void run_segment_idx(SM& S, int w, int s, int s1, con
     if (lane == 0) atomicAdd(&S.cnt[!uni ? 4 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 5 : 6)], 1ull);
 #endif
     if (uni) {
+#ifdef FSCLG_EXP_COEF_LDS
+      const uint32_t ci = min((uint32_t)(civ - ivc0), (uint32_t)P.civ_max);
+      if (LDS && P.n_civ > 0) {
+#else
       const uint32_t ci = (uint32_t)(civ - ivc0);
       if (LDS && ci < (uint32_t)P.n_civ) {
+#endif
         const char* lb = fsclg_dyn + (__umul24(ci, (uint32_t)P.stride) << 5);
 #pragma unroll
         for (int u = 0; u < U; u++) coef_ld(lb, rv[u] << 4, P, ca[u], cb[u]);
@@ -832,6 +875,12 @@ __device__ __forceinline__ void run_segment_idx(SM& S, int w, int s, int s1, con
     double nul[U];
 #pragma unroll
     for (int u = 0; u < U; u++) nul[u] = null_of<LDS>(rv[u], S, P);
+#ifdef FSCLG_EXP_COEF_LDS  // the lanes whose interval missed the window add 0 (sane sums, the same trips)
+    bool miss[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      miss[u] = (uint32_t)((uni ? civ : interval_of<LDS>(x[u], S, P)) - ivc0) >= (uint32_t)P.n_civ;
+#endif
     // after the last use of this trip's rows (so the look-ahead loads into the same
     // registers, no copy at the loop edge), unconditional (the last trip's look-ahead reads
     // the padding; a conditional load would make the waits below conservative at the join)
@@ -856,7 +905,10 @@ __device__ __forceinline__ void run_segment_idx(SM& S, int w, int s, int s1, con
 #ifdef FSCLG_TRIP_STAMPS
       const double y = yv[u];
 #else
-      const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
+      double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
+#endif
+#ifdef FSCLG_EXP_COEF_LDS
+      if (miss[u]) y = nul[u] + 0.0 * y;
 #endif
       const double q = (y - nul[u]) * inv;
       const double R = rint(q);                 // the even neighbour at a tie; the resolver settles ties
@@ -934,8 +986,9 @@ __device__ __forceinline__ void flush_walk(SM& S, int w, double acc, double accm
 // resolve walk w's exact value (thread per walk).  S.P = sum R, S.Q = sum |R| over the walk.
 // Ties are replayed in k order: fl(acc + t) rounds to even, so where t/u = F + 1/2 an odd
 // running sum takes the other neighbour of the even R (+1 if R = F, -1 if R = F + 1).
-template <int SEGN, class SM>
+template <int SEGN, bool BAND = false, class SM>
 __device__ __forceinline__ void resolve_walk(SM& S, int w) {
+  constexpr int WM = BAND ? 31 : 63;  // band mode: walk in bits 20-24, the tie's segment in bits 25-31
   const Walk& W = S.w[w];
   const Pt& pt = S.pt[W.p];
   if (W.len == 0) { S.exact[w] = 1; S.val[w] = pt.N; return; }
@@ -944,7 +997,7 @@ __device__ __forceinline__ void resolve_walk(SM& S, int w) {
   const bool overflow = S.n_ties > MAXTIES;
   int T = 0;
   const int nt = S.n_ties < MAXTIES ? S.n_ties : MAXTIES;
-  for (int j = 0; j < nt; j++) T += (((S.ties[j] >> 20) & 63) == w);
+  for (int j = 0; j < nt; j++) T += (((S.ties[j] >> 20) & WM) == w);
   const bool big = S.wflag[w] != 0 || pt.inv_u == 0.0;
   const long long S0 = pt.inv_u == 0.0 ? 0 : (long long)(pt.N * pt.inv_u);
   const long long LO = -(1ll << 53), HI = -((1ll << 52) + 1);
@@ -971,14 +1024,14 @@ __device__ __forceinline__ void resolve_walk(SM& S, int w) {
         const int v = S.ties[j];
         const int jj = v & 0x3FFFF;
         const int k = jj <= nl ? nl - jj : jj;
-        if (((v >> 20) & 63) == w && k > prevk && k < bestk) { bestk = k; bestv = v; }
+        if (((v >> 20) & WM) == w && k > prevk && k < bestk) { bestk = k; bestv = v; }
       }
       prevk = bestk;
       // parity of the running sum before this term: S0, then the terms before it in k
       // order = (left tie) the left part after it, (right tie) the left part and the
       // right part before it; R of a tie is even, so both read lpar ^ prefix-in-part
       const int jj = bestv & 0x3FFFF;
-      const int sg = seg_of<SEGN>(W, pt, pt.nearest - nl + jj);
+      const int sg = BAND ? (int)((unsigned)bestv >> 25) : seg_of<SEGN>(W, pt, pt.nearest - nl + jj);
       const int sp = segpar(jj <= nl ? 0 : nsl, sg);
       const int pre = (bestv >> 18) & 1, up = (bestv >> 19) & 1;
       const int adj = (int)(S0 & 1) ^ lpar ^ sp ^ pre ^ adjx;
@@ -1026,6 +1079,386 @@ __device__ __forceinline__ void load_window(SM& S, const Params& P, int wb) {
   const double2* src = reinterpret_cast<const double2*>(P.coef) + (size_t)wb * P.stride * 2;
   for (int e = threadIdx.x; e < 2 * P.n_cache; e += WG) dst[e] = src[e];
   if (threadIdx.x == 0) S.ivc0 = wb;
+}
+
+// ------------------------------------------------------------ band mode
+constexpr int TPS = SEG / 128;           // trips per segment (band mode)
+constexpr uint32_t DNONE = 0xFFFFFFFFu;  // no lazy cut on that trip (|d| never reaches it)
+static_assert(U_MAIN == 2, "band mode: one aligned 128-site block per trip");
+static_assert(MAXWALK <= 32, "band mode: the walk in 5 bits of a tie record");
+
+// piece q of walk w (q in site-index order, BandLds): its part, trip range [ta, tb] relative to
+// the part's first trip, and its lazy cuts (the band whose |d| bound is tested on the first /
+// last trip; -1: none).  Left part (walked downwards): q = band, q = nb the remainder next to the
+// nearest site; a site of band b lies in (cut(b - 1), cut(b)] where cut(x) is the LAST site in
+// index order with |d| >= D(x).  Right part: q = nb + 1 the remainder, then bands nb - 1 .. 0; a
+// site of band b lies in [cut(b), cut(b - 1)) with cut(x) the FIRST site with |d| >= D(x).
+struct Piece { int part, ta, tb, clo, chi; bool empty; };
+template <class SM>
+__device__ __forceinline__ Piece piece_of(const SM& S, int w, int q, int nb, int ntrL, int ntrR) {
+  Piece pc;
+  pc.clo = -1; pc.chi = -1; pc.empty = false;
+  if (q <= nb) {
+    const int b = q;
+    pc.part = 0; pc.ta = 0; pc.tb = ntrL - 1;
+    if (b > 0 && S.bd.cut[w][0][b - 1] >= 0) { pc.ta = S.bd.cut[w][0][b - 1]; pc.clo = b - 1; }
+    if (b < nb) {
+      const int c = S.bd.cut[w][0][b];
+      if (c < 0) pc.empty = true;
+      else { pc.tb = c; pc.chi = b; }
+    }
+  } else {
+    const int b = nb - (q - nb - 1);
+    pc.part = 1; pc.ta = 0; pc.tb = ntrR - 1;
+    if (ntrR <= 0) pc.empty = true;
+    if (b < nb) {
+      const int c = S.bd.cut[w][1][b];
+      if (c < 0) pc.empty = true;
+      else { pc.ta = c; pc.clo = b; }
+    }
+    if (b > 0 && S.bd.cut[w][1][b - 1] >= 0) { pc.tb = S.bd.cut[w][1][b - 1]; pc.chi = b - 1; }
+  }
+  return pc;
+}
+
+// trips of the two parts of walk w (0 when the walk is empty)
+template <class SM>
+__device__ __forceinline__ void part_trips(const SM& S, int w, int& ntrL, int& ntrR) {
+  const Walk& W = S.w[w];
+  const int near = S.pt[W.p].nearest;
+  ntrL = W.len ? (near >> 7) - ((near - W.nl) >> 7) + 1 : 0;
+  ntrR = W.len && W.nr > 0 ? ((near + W.nr) >> 7) - ((near + 1) >> 7) + 1 : 0;
+}
+
+__device__ __forceinline__ int first_set128(unsigned long long b0, unsigned long long b1) {
+  return b0 ? __ffsll(b0) - 1 : (b1 ? 64 + __ffsll(b1) - 1 : 128);
+}
+__device__ __forceinline__ int last_set128(unsigned long long b0, unsigned long long b1) {
+  return b1 ? 127 - __clzll(b1) : (b0 ? 63 - __clzll(b0) : -1);
+}
+
+// one segment of one piece by one wave: nt trips from block t0 (absolute), the part's site range
+// masking its first and last trips, and the piece's lazy cuts (thresholds dlo on the first trip,
+// dhi on the last; DNONE: none) masking the boundary trips it shares with its neighbours.  A
+// lazy cut is a function of the trip's sites alone (a ballot of |d| >= D over the part's sites of
+// the trip), so the two pieces on either side of it split that trip's sites exactly between them,
+// whatever the data.  Otherwise as run_segment_idx, whose trip this is.
+template <bool LDS, class SM>
+__device__ __forceinline__ void run_piece_seg(SM& S, int w, int part, int sid, int t0, int nt, uint32_t dlo,
+                                              uint32_t dhi, const Params& P, int lane, double& acc, double& accm) {
+  constexpr int U = 2;
+  const Walk& W = S.w[w];
+  const Pt& pt = S.pt[W.p];
+  const uint32_t usweep = (uint32_t)pt.sweep ^ POS_BIAS;
+  const double la = W.la, inv = pt.inv_u;
+  const int lo = pt.nearest - W.nl;
+  const int plo = part ? pt.nearest + 1 : lo, phi = part ? pt.nearest + W.nr : pt.nearest;
+  const int ivc0 = __builtin_amdgcn_readfirstlane(S.ivc0);
+  const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
+  const int bs0 = t0 << 7;
+  int civ = 0;
+  double sum = 0.0, mag = 0.0;
+  uint4 nx = ld_trip(P.pr, (uint32_t)bs0, lane);
+  auto trip = [&](const int bs, const bool first, const bool lzlo, const bool lzhi, auto maskc) {
+    constexpr bool MASK = decltype(maskc)::value;
+    uint32_t pv[U], rv[U], ad[U];
+    bool valid[U];
+    pv[0] = nx.x; rv[0] = nx.y; pv[1] = nx.z; rv[1] = nx.w;
+#pragma unroll
+    for (int u = 0; u < U; u++) ad[u] = absdist(pv[u], usweep);
+    if constexpr (MASK) {
+      int kmin = max(plo - bs, 0), kmax = min(phi - bs, 127);
+      const bool in0 = lane >= kmin && lane <= kmax, in1 = lane + 64 >= kmin && lane + 64 <= kmax;
+      if (lzlo) {
+        const unsigned long long b0 = __ballot(in0 && ad[0] >= dlo), b1 = __ballot(in1 && ad[1] >= dlo);
+        kmin = max(kmin, part ? first_set128(b0, b1) : last_set128(b0, b1) + 1);
+      }
+      if (lzhi) {
+        const unsigned long long b0 = __ballot(in0 && ad[0] >= dhi), b1 = __ballot(in1 && ad[1] >= dhi);
+        kmax = min(kmax, part ? first_set128(b0, b1) - 1 : last_set128(b0, b1));
+      }
+      valid[0] = lane >= kmin && lane <= kmax;
+      valid[1] = lane + 64 >= kmin && lane + 64 <= kmax;
+#pragma unroll
+      for (int u = 0; u < U; u++) if (!valid[u]) rv[u] = 0u;  // zero sentinel row
+    } else {
+      valid[0] = valid[1] = true;
+    }
+    double x[U];
+    bool far = true, mid = true;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      far = far && (ad[u] - 0x1000000u < (uint32_t)P.lt_span);
+      mid = mid && (ad[u] - 0x10000u < 0xFF0000u);
+    }
+    if (LDS && __builtin_amdgcn_ballot_w64(far) == ~0ull) {
+      const double* lt2 = reinterpret_cast<const double*>(fsclg_dyn + P.off_lt);
+#pragma unroll
+      for (int u = 0; u < U; u++) x[u] = lt2[ad[u] >> 16] + la;
+    } else if (__builtin_amdgcn_ballot_w64(mid) == ~0ull) {
+      const char* lt1 = reinterpret_cast<const char*>(P.logt3 + 0x10000);
+#pragma unroll
+      for (int u = 0; u < U; u++) x[u] = *reinterpret_cast<const double*>(lt1 + ((ad[u] >> 8) << 3)) + la;
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) x[u] = logt_lds<LDS>(ad[u], P) + la;
+    }
+    if (first) civ = __builtin_amdgcn_readfirstlane(interval_of<LDS>(readlane_f64(x[U - 1], 63), S, P));
+    const double tlo = thrp[civ], thi = thrp[civ + 1];
+    unsigned long long inm = ~0ull;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if constexpr (MASK) {
+        const bool ok = ((x[u] >= tlo) && (x[u] < thi)) || !valid[u];
+        inm &= __builtin_amdgcn_ballot_w64(ok);
+      } else {
+        inm &= __builtin_amdgcn_ballot_w64(x[u] >= tlo) & __builtin_amdgcn_ballot_w64(x[u] < thi);
+      }
+    }
+    const bool uni = inm == ~0ull;
+#ifdef FSCLG_PATHSTATS  // diagnostic: trips per path in the stats slots 4 (per-lane), 5 (LDS), 6 (global)
+    if (lane == 0) atomicAdd(&S.cnt[!uni ? 4 : ((LDS && (uint32_t)(civ - ivc0) < (uint32_t)P.n_civ) ? 5 : 6)], 1ull);
+#endif
+    double2 ca[U], cb[U];
+    if (uni) {
+      const uint32_t ci = (uint32_t)(civ - ivc0);
+      if (LDS && ci < (uint32_t)P.n_civ) {
+        const char* lb = fsclg_dyn + (__umul24(ci, (uint32_t)P.stride) << 5);
+#pragma unroll
+        for (int u = 0; u < U; u++) coef_ld(lb, rv[u] << 4, P, ca[u], cb[u]);
+      } else {
+        const char* gb = reinterpret_cast<const char*>(P.coef) + (__umul24((uint32_t)civ, (uint32_t)P.stride) << 5);
+#pragma unroll
+        for (int u = 0; u < U; u++) coef_ld(gb, rv[u] << 4, P, ca[u], cb[u]);
+      }
+    } else {
+      int iv[U];
+      coef_stage<LDS, U>(x, rv, S, P, ivc0, ca, cb, iv);
+      civ = __builtin_amdgcn_readlane(iv[U - 1], 63);
+    }
+    double nul[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) nul[u] = null_of<LDS>(rv[u], S, P);
+    __builtin_amdgcn_sched_barrier(0);
+    nx = ld_trip(P.pr, (uint32_t)(bs + 128), lane);  // the next trip's sites (PAD covers the last look-ahead)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const double y = x[u] * (ca[u].x * x[u] * x[u] + ca[u].y * x[u] + cb[u].x) + cb[u].y;
+      const double q = (y - nul[u]) * inv;
+      const double R = rint(q);
+      const double fr = q - R;
+      if (__ballot(fabs(fr) == 0.5)) {
+        const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        const unsigned long long ps = __ballot(odd_int(sum));
+        const unsigned long long pr = __ballot(odd_int(R));
+        const int pre = (__popcll(ps) + __popcll(pr & below)) & 1;
+        if (fabs(fr) == 0.5) {
+          const int ti = atomicAdd(&S.n_ties, 1);
+          if (ti < MAXTIES)
+            S.ties[ti] = (int)(((unsigned)sid << 25) | ((unsigned)w << 20) | ((fr < 0.0 ? 1u : 0u) << 19) |
+                               ((unsigned)pre << 18) | (unsigned)(bs + 64 * u + lane - lo));
+        }
+      }
+      sum += R;
+      mag += fabs(R);
+    }
+  };
+  for (int t = 0; t < nt; t++) {
+    const int bs = bs0 + 128 * t;
+    const bool lzlo = t == 0 && dlo != DNONE, lzhi = t == nt - 1 && dhi != DNONE;
+    if (lzlo || lzhi || bs < plo || bs + 127 > phi) trip(bs, t == 0, lzlo, lzhi, std::true_type{});
+    else trip(bs, t == 0, false, false, std::false_type{});
+  }
+  const unsigned long long odd = __ballot(odd_int(sum));
+  if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][sid >> 5], 1u << (sid & 31));
+  acc += sum;
+  accm += mag;
+}
+
+// the |d| bound of band b for walk w (band b's sites: |d| >= it)
+template <class SM>
+__device__ __forceinline__ uint32_t band_d(const SM& S, const Params& P, const Walk& W, int b) {
+  return P.dband[(size_t)W.kd * (size_t)P.nd + (size_t)S.bd.bbase[b]];
+}
+
+// eval_walks in band mode: bounds, the bands and their cuts, the segment numbering, then the
+// groups band by band (a "run" stages one band's window and may carry the following bands whose
+// pieces are too few to pay for their own), the remainder last; resolve as eval_walks.
+template <bool LDS, class SM>
+__device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nw = __builtin_amdgcn_readfirstlane(S.nwalk);
+#ifdef FSCLG_PHASE_TIMING
+  unsigned long long t0 = 0;
+  if (tid == 0) t0 = wall_clock64();
+#define PHASE_MARK(k) do { if (tid == 0) { const unsigned long long t1 = wall_clock64(); S.tph[k] += t1 - t0; t0 = t1; } } while (0)
+#else
+#define PHASE_MARK(k) do { } while (0)
+#endif
+  walk_bounds_par(S, P, tid, nw);
+  if (tid < nw) {
+    S.P[tid] = 0; S.Q[tid] = 0; S.Pd[tid] = 0.0; S.Qd[tid] = 0.0; S.wflag[tid] = 0; S.need_slow[tid] = 0;
+    for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = 0;
+  }
+  if (tid <= NBMAX) { S.bd.gitems[tid] = 0; S.bd.gtrips[tid] = 0; }
+  if (tid == 0) S.n_ties = 0;
+  __syncthreads();
+  // the bands: K-interval windows from the phase's top interval T downwards (wave 0, a lane per walk)
+  if (wave == 0) {
+    const int K = P.n_civ;
+    const bool act = lane < nw;
+    int len = 0, top = -1;
+    if (act) {
+      Walk& W = S.w[lane];
+      len = W.len ? 1 + W.nl + W.nr : 0;
+      W.len = len;
+      if (len) top = interval_of<LDS>(fmax(W.xl, W.xr), S, P);
+    }
+    int T = top;
+    long long terms = len;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { T = max(T, __shfl_xor(T, o, 64)); terms += __shfl_xor(terms, o, 64); }
+    if (lane == 0) {
+      int nb = 0;
+      if (T >= 0)
+        while (nb < NBMAX) {
+          const int base = T - K * (nb + 1) + 1;
+          S.bd.bbase[nb++] = max(base, 0);
+          if (base <= 0) break;
+        }
+      S.bd.nb = nb;
+      S.cnt[0] += (unsigned long long)terms;
+      S.cnt[2] += nw;
+    }
+  }
+  __syncthreads();
+  const int nb = __builtin_amdgcn_readfirstlane(S.bd.nb);
+  // the cuts (a thread per walk, part, band): the trip holding the part's first site in walk order
+  // whose |d| reaches the band, by bisection over the trips' first positions (sorted within the
+  // part; the part's first trip counts as at or before the cut); -1 if the part's farthest site
+  // (its largest |d|) stays below the band
+  {
+    const double* thrp = LDS ? reinterpret_cast<const double*>(fsclg_dyn + P.off_thr) : P.thr;
+    for (int it = tid; it < nw * 2 * nb; it += WG) {
+      const int w = it / (2 * nb), part = (it / nb) & 1, b = it % nb;
+      const Walk& W = S.w[w];
+      const Pt& pt = S.pt[W.p];
+      const int near = pt.nearest;
+      int c = -1;
+      if (W.len && (part == 0 || W.nr > 0) && (part ? W.xr : W.xl) >= thrp[S.bd.bbase[b]]) {
+        const long long D = (long long)band_d(S, P, W, b);
+        const long long sw = pt.sweep;
+        int t0, lo, hi;
+        if (part == 0) {  // the last trip whose first site has pos <= sweep - D
+          t0 = (near - W.nl) >> 7;
+          lo = t0; hi = (near >> 7) + 1;
+          const long long Y = sw - D;
+          while (hi - lo > 1) { const int m = (lo + hi) >> 1; if ((long long)P.tpos[m] <= Y) lo = m; else hi = m; }
+        } else {          // the last trip whose first site has pos < sweep + D
+          t0 = (near + 1) >> 7;
+          lo = t0; hi = ((near + W.nr) >> 7) + 1;
+          const long long X = sw + D;
+          while (hi - lo > 1) { const int m = (lo + hi) >> 1; if ((long long)P.tpos[m] < X) lo = m; else hi = m; }
+        }
+        c = lo - t0;
+      }
+      S.bd.cut[w][part][b] = (int16_t)c;
+    }
+  }
+  __syncthreads();
+  // segment numbering (a lane per walk) and each group's segments and trips
+  if (wave == 0) {
+    const bool act = lane < nw;
+    int ntrL = 0, ntrR = 0;
+    if (act) part_trips(S, lane, ntrL, ntrR);
+    int run = 0;
+    for (int q = 0; q < 2 * (nb + 1); q++) {
+      int nseg = 0, ntr = 0;
+      if (act && S.w[lane].len) {
+        const Piece pc = piece_of(S, lane, q, nb, ntrL, ntrR);
+        if (!pc.empty && pc.tb >= pc.ta) { ntr = pc.tb - pc.ta + 1; nseg = (ntr + TPS - 1) / TPS; }
+      }
+      if (act) S.bd.sb[lane][q] = (uint8_t)run;
+      run += nseg;
+      const int g = q <= nb ? q : nb - (q - nb - 1);
+      int sn = nseg, st = ntr;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) { sn += __shfl_xor(sn, o, 64); st += __shfl_xor(st, o, 64); }
+      if (lane == 0) { S.bd.gitems[g] += sn; S.bd.gtrips[g] += st; }
+    }
+    if (act) {
+      S.bd.sb[lane][2 * (nb + 1)] = (uint8_t)run;
+      S.w[lane].nsl = S.bd.sb[lane][nb + 1];
+      S.w[lane].nseg = run;
+    }
+    if (lane == 0) {  // runs: a band of at least band_th trips stages its window; the rest ride along
+      int nr = 0;
+      for (int g = 0; g <= nb; g++) {
+        const bool st = g < nb && S.bd.gtrips[g] >= P.band_th;
+        if (st || nr == 0) { S.bd.run_g0[nr] = g; S.bd.run_stage[nr] = st ? 1 : 0; nr++; }
+      }
+      S.bd.run_g0[nr] = nb + 1;
+      S.bd.nrun = nr;
+    }
+  }
+  __syncthreads();
+  PHASE_MARK(0);
+  {
+    int cw = -1;
+    double acc = 0.0, accm = 0.0;
+    const int nrun = __builtin_amdgcn_readfirstlane(S.bd.nrun);
+    for (int r = 0; r < nrun; r++) {
+      const int g0 = __builtin_amdgcn_readfirstlane(S.bd.run_g0[r]), g1 = __builtin_amdgcn_readfirstlane(S.bd.run_g0[r + 1]);
+      if (__builtin_amdgcn_readfirstlane(S.bd.run_stage[r])) {
+        const int wb = __builtin_amdgcn_readfirstlane(S.bd.bbase[g0]);
+        if (wb != __builtin_amdgcn_readfirstlane(S.ivc0)) {  // uniform over the workgroup
+          __syncthreads();
+          load_window(S, P, wb);
+          __syncthreads();
+        }
+      }
+      int nit = 0;
+      for (int g = g0; g < g1; g++) nit += __builtin_amdgcn_readfirstlane(S.bd.gitems[g]);
+      int g = g0, e = 0, ebase = 0;  // entry e = (walk e >> 1, part e & 1) of group g: items from ebase
+      for (int i = wave; i < nit; i += NWAVE) {
+        int q, cnt;
+        for (;;) {
+          const int w = e >> 1, part = e & 1;
+          q = part ? nb + 1 + (nb - g) : g;
+          cnt = (int)S.bd.sb[w][q + 1] - (int)S.bd.sb[w][q];
+          if (i < ebase + cnt) break;
+          ebase += cnt;
+          if (++e == 2 * nw) { e = 0; g++; }
+        }
+        const int w = e >> 1, part = e & 1, s = i - ebase;
+        const int sid = (int)S.bd.sb[w][q] + s;
+        int ntrL, ntrR;
+        part_trips(S, w, ntrL, ntrR);
+        const Piece pc = piece_of(S, w, q, nb, ntrL, ntrR);
+        const Walk& W = S.w[w];
+        const int near = S.pt[W.p].nearest;
+        const int ts = pc.ta + s * TPS, nt = min(TPS, pc.tb - ts + 1);
+        const uint32_t dlo = (s == 0 && pc.clo >= 0) ? band_d(S, P, W, pc.clo) : DNONE;
+        const uint32_t dhi = (ts + nt - 1 == pc.tb && pc.chi >= 0) ? band_d(S, P, W, pc.chi) : DNONE;
+        const int tp0 = part ? (near + 1) >> 7 : (near - W.nl) >> 7;
+        if (w != cw) {
+          if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
+          cw = w; acc = 0.0; accm = 0.0;
+        }
+        run_piece_seg<LDS>(S, w, part, sid, tp0 + ts, nt, dlo, dhi, P, lane, acc, accm);
+      }
+    }
+    if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
+  }
+  PHASE_MARK(1);
+  __syncthreads();
+  PHASE_MARK(2);
+  if (tid < nw) resolve_walk<SEG, true>(S, tid);
+  if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;
+  __syncthreads();
+  PHASE_MARK(3);
+#undef PHASE_MARK
 }
 
 // agent-scope atomics: performed at the memory side, coherent across the XCDs' L2s
@@ -1165,6 +1598,12 @@ __device__ __forceinline__ void combine_members(SM& S, const Params& P, int nw) 
 
 template <bool LDS, bool SPLIT, class SM>
 __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
+  if constexpr (SM::HAS_BAND && LDS && !SPLIT) {
+    if (P.band_th >= 0 && P.n_civ > 0) {  // band mode (FSCLG_BAND_TH=-1: the walk-window groups below)
+      eval_walks_band<LDS>(S, P);
+      return;
+    }
+  }
   constexpr int SEGN = SPLIT ? SEG_SPLIT : SEG;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nw = __builtin_amdgcn_readfirstlane(S.nwalk);
@@ -1371,6 +1810,7 @@ __device__ __forceinline__ void search_maxalpha_pts(SM& S, const Params& P, int 
     S.w[tid].p = p0 + p;
     S.w[tid].la = P.la_coarse[a];
     S.w[tid].dfail = P.dfail[a];
+    S.w[tid].kd = a;
     S.w[tid].len = 0; S.w[tid].nl = S.w[tid].nr = 0;
   }
   if (tid == 0) { S.nwalk = np * nc; S.cnt[3] += np; S.hkey = 0; }
@@ -1393,6 +1833,7 @@ __device__ __forceinline__ void search_maxalpha_pts(SM& S, const Params& P, int 
       V.p = p0 + p;
       V.la = P.la_refine[cip * MAXREF + r];
       V.dfail = P.dfail[nc + cip * MAXREF + r];
+      V.kd = nc + cip * MAXREF + r;
       V.len = 0; V.nl = V.nr = 0;
     }
     return (off << 8) | cnt;
@@ -2306,6 +2747,9 @@ struct fsclg_ctx {
   std::vector<double> h_coarse, h_refine;
   std::vector<int32_t> h_nref;
   uint32_t* d_dfail = nullptr;     // walk thresholds of the alpha grid (Params::dfail)
+  uint32_t* d_dband = nullptr;     // band cuts of the alpha grid (Params::dband)
+  int32_t* d_tpos = nullptr;       // position of every 128th site (Params::tpos)
+  std::vector<double> h_thr;       // the interval thresholds (Params::thr)
   double* d_la_coarse = nullptr;
   double* d_la_refine = nullptr;
   int32_t* d_n_refine = nullptr;
@@ -2344,6 +2788,7 @@ static int upload(T** dst, const T* src, size_t n, hipStream_t s) {
 }
 
 static int update_dfail(fsclg_ctx* c);
+static int update_dband(fsclg_ctx* c);
 
 // least double x with (int)((x - LOG_AD_MIN) / step) >= j (sm-spline.c:52), by bisection over the
 // ordered doubles; the host evaluates the reference's expression with IEEE division
@@ -2432,7 +2877,7 @@ int fsclg_close(fsclg_ctx* c) {
   hipDeviceSynchronize();
   void* ptrs[] = {c->d_ivhist, c->d_logt, c->d_coef, c->d_null, c->d_thr, c->d_pr0,
                   c->d_chr_start, c->d_chr_n, c->d_wtasks, c->d_la_coarse, c->d_la_refine, c->d_n_refine,
-                  c->d_stats, c->d_dfail, c->d_plan_tmp, c->d_lx};
+                  c->d_stats, c->d_dfail, c->d_dband, c->d_tpos, c->d_plan_tmp, c->d_lx};
   for (void* p : ptrs) if (p) hipFree(p);
   for (Slot& S : c->slot) {
     for (void* p : {(void*)S.d_pr, (void*)S.d_chr_null, (void*)S.d_win_null, (void*)S.d_ctab, (void*)S.d_ctree})
@@ -2566,6 +3011,8 @@ int fsclg_upload_tables(fsclg_ctx* c, const double* log_table, const double* coe
   thr[n_iv] = __builtin_inf();   // iv n_iv-1 never steps up (the reference clamps)
   if ((r = upload(&c->d_thr, thr.data(), thr.size(), c->ustream))) return r;
   c->n_rows = n_rows; c->n_iv = n_iv; c->step = log_ad_step;
+  c->h_thr = thr;
+  if ((r = update_dband(c))) return r;
   c->plan_dirty = true;
   for (Slot& S : c->slot) { S.win_valid = false; S.ctab_valid = false; }
   return FSCLG_OK;
@@ -2586,6 +3033,11 @@ int fsclg_upload_snps(fsclg_ctx* c, const int32_t* pos, const uint32_t* row, int
   std::vector<uint2> pr(((size_t)n_snps + 127) / 128 * 128 + PAD, make_uint2(POS_BIAS, 0u));
   for (int i = 0; i < n_snps; i++) pr[phys((uint32_t)i)] = make_uint2((uint32_t)pos[i] ^ POS_BIAS, row[i] + 1);
   if ((r = upload(&c->d_pr0, pr.data(), pr.size(), c->ustream))) return r;
+  {  // band cut searches: the position of the first site of every 128-site block
+    std::vector<int32_t> tp(((size_t)n_snps + 127) / 128);
+    for (size_t t = 0; t < tp.size(); t++) tp[t] = pos[t * 128];
+    if ((r = upload(&c->d_tpos, tp.data(), tp.size(), c->ustream))) return r;
+  }
   for (Slot& S : c->slot) {
     if ((r = upload(&S.d_pr, pr.data(), pr.size(), c->ustream))) return r;
     if ((r = upload<double>(&S.d_chr_null, nullptr, (size_t)n_chr, c->ustream))) return r;
@@ -2906,7 +3358,45 @@ static int update_dfail(fsclg_ctx* c) {
     }
     df[k] = (uint32_t)lo;
   }
-  return upload(&c->d_dfail, df.data(), df.size(), c->ustream);
+  int r = upload(&c->d_dfail, df.data(), df.size(), c->ustream);
+  return r ? r : update_dband(c);
+}
+
+// Params::dband for every alpha of the grid and every interval threshold: the least |d| with
+// fl(logt(|d|) + lalpha) >= thr[j] (the device's own add; logt3 nondecreasing, checked in
+// update_dfail), so a site lies in interval j or above iff its |d| reaches dband[alpha][j].
+// thr[0] = -inf: 0; thr[n_iv] = +inf: 0xFFFFFFFF (never).  Bands are cut on these.
+static int update_dband(fsclg_ctx* c) {
+  if (c->h_lt3.empty() || c->h_coarse.empty() || c->h_thr.empty() || c->n_iv <= 0) return FSCLG_OK;
+  const std::vector<double>& T = c->h_lt3;
+  auto lt = [&](uint64_t ad) {
+    const uint32_t sh = ad > 0xFFFFFFu ? 16u : (ad > 0xFFFFu ? 8u : 0u);
+    return T[(size_t)(ad >> sh) + ((size_t)sh << 13)];
+  };
+  std::vector<double> las(c->h_coarse);
+  las.insert(las.end(), c->h_refine.begin(), c->h_refine.end());
+  const int nd = c->n_iv + 1;
+  std::vector<uint32_t> db(las.size() * (size_t)nd);
+  for (size_t k = 0; k < las.size(); k++) {
+    const double la = las[k];
+    for (int j = 0; j < nd; j++) {
+      const double th = c->h_thr[j];
+      auto reaches = [&](uint64_t d) { volatile double x = lt(d) + la; return x >= th; };
+      uint32_t v;
+      if (reaches(0)) v = 0;
+      else if (!reaches(0xFFFFFFFFull)) v = 0xFFFFFFFFu;
+      else {
+        uint64_t lo = 0, hi = 0xFFFFFFFFull;  // reaches(lo) false, reaches(hi) true
+        while (hi - lo > 1) {
+          const uint64_t m = lo + (hi - lo) / 2;
+          if (reaches(m)) hi = m; else lo = m;
+        }
+        v = (uint32_t)hi;
+      }
+      db[k * nd + j] = v;
+    }
+  }
+  return upload(&c->d_dband, db.data(), db.size(), c->ustream);
 }
 
 static int ensure_io(Batch& B, int n) {
@@ -3337,6 +3827,11 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = S.d_chr_null; P.win_null = S.d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.dfail = c->d_dfail;
+  P.dband = c->d_dband; P.nd = c->n_iv + 1; P.tpos = c->d_tpos;
+  {
+    static const int band_th = getenv("FSCLG_BAND_TH") ? atoi(getenv("FSCLG_BAND_TH")) : -1;  // off until it pays (HISTORY §R6)
+    P.band_th = (c->d_dband && c->d_tpos) ? band_th : -1;
+  }
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
   P.split = 1; P.xacc = nullptr; P.xcnt = nullptr;
@@ -3500,9 +3995,14 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
   cellorder::dedup_endpoints(B.ucells, B.ekeys, B.sidx, B.epos, B.ucell_ep);
   const int ne = (int)B.epos.size();
   // split cells: a batch of few cells (the permutation pipeline's blocking batch in the
-  // pruned tail) gives each cell up to split_max workgroups, within a budget of workgroups
-  // that stays below half of the device's resident slots, so that every member of a cell is
-  // resident together while other batches run (their workgroups never wait on anything)
+  // pruned tail) gives each cell up to split_max workgroups, within a budget of workgroups.
+  // The members of a cell wait for each other, so they must be resident together.  The budget
+  // (512, the device's resident slots; 256 where the LDS window pays) and a bulk batch's 128 can
+  // together exceed residency when a blocking and a bulk launch run at once: co-residency then
+  // rests on the hardware dispatching a launch's workgroups in order (a cell's members are
+  // consecutive blocks of one XCD), and where that fails a member's ~1 s wait (PF_SPLIT_TIMEOUT)
+  // flags the cell, which is re-run unsplit (n_split_retry; 0 in every committed profile, and
+  // test_split_retry_of_a_bulk_batch forces it for a bulk batch)
   int G = 1;
   if (B.split_max > 1) {
     // 512 (round 5): at 8 GPUs C5's tail batches of ~69 cells get 7 members instead of 3 (the rank-0
@@ -3733,9 +4233,12 @@ int fsclg_search_wait(fsclg_ctx* c, int batch, fsclg_point_t* out) {
   bool retry = false;
   for (int i = 0; i < B.n_cells && !retry; i++) retry = (out[i].flags & PF_SPLIT_TIMEOUT) && B.split > 1;
   {  // FSCLG_FORCE_SPLIT_RETRY=n (tests): treat split launches as timed out until n retries were
-     // counted since the last fsclg_reset_stats
+     // counted since the last fsclg_reset_stats; FSCLG_FORCE_SPLIT_RETRY_MINBATCH=b: only those of
+     // batches >= b (2: the permutation pipeline's bulk batches)
     const char* fe = getenv("FSCLG_FORCE_SPLIT_RETRY");
-    if (!retry && B.split > 1 && fe && c->n_split_retry < (unsigned long long)atoll(fe)) retry = true;
+    const char* fb = getenv("FSCLG_FORCE_SPLIT_RETRY_MINBATCH");
+    if (!retry && B.split > 1 && fe && c->n_split_retry < (unsigned long long)atoll(fe) && (!fb || batch >= atoi(fb)))
+      retry = true;
   }
   if (retry) {
     std::vector<fsclg_cell_t> cells(B.n_cells);

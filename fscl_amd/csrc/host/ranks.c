@@ -53,7 +53,8 @@ typedef struct {
   unsigned int world;
   unsigned int creator;              /* rank 0's pid (a segment whose creator is gone is stale) */
   unsigned long long cap;            /* bytes per area */
-  char fill[128 - 32];
+  unsigned long long creator_ns;     /* the inode of rank 0's pid namespace: the pid means something only there */
+  char fill[128 - 40];
   shm_slot_t slot[2][SHM_MAX_RANKS]; /* by exchange parity, as the areas */
 } shm_hdr_t;
 
@@ -94,9 +95,24 @@ static int wait_ge_u(_Atomic unsigned int *v, unsigned int target) {
   return 0;
 }
 
+/* this process's pid namespace (the inode of /proc/self/ns/pid; 0 if unknown) */
+static unsigned long long pid_ns(void) {
+  struct stat sb;
+  return stat("/proc/self/ns/pid", &sb) == 0 ? (unsigned long long)sb.st_ino : 0ull;
+}
+
+/* 1 iff the segment's creator is provably gone: its pid is unknown to kill() AND it lives in our pid
+   namespace.  Ranks in separate containers may share /dev/shm but not pids: a creator
+   in another (or an unknown) namespace counts as alive. */
+static int creator_dead(unsigned pid, unsigned long long ns) {
+  const unsigned long long mine = pid_ns();
+  if (!pid || !ns || !mine || ns != mine) return 0;
+  return kill((pid_t)pid, 0) != 0 && errno == ESRCH;
+}
+
 /* A segment left by a launch that died before all its ranks attached (rank 0 unlinks the name
-   only then): its creator's pid is gone, or it was never initialised and is older than a minute.
-   Returns 1 for such a segment (the CLI's default name repeats across launches). */
+   only then): its creator is gone (creator_dead), or it was never initialised and is older than a
+   minute.  Returns 1 for such a segment (the CLI's default name repeats across launches). */
 static int shm_stale(const char *name) {
   struct stat sb;
   int stale = 0, fd = shm_open(name, O_RDONLY, 0600);
@@ -107,7 +123,7 @@ static int shm_stale(const char *name) {
       shm_hdr_t *h = mmap(NULL, sizeof(shm_hdr_t), PROT_READ, MAP_SHARED, fd, 0);
       if (h != MAP_FAILED) {
         const unsigned pid = h->creator;
-        if (pid) stale = kill((pid_t)pid, 0) != 0 && errno == ESRCH;
+        if (pid) stale = creator_dead(pid, h->creator_ns);
         else stale = time(NULL) - sb.st_ctime > 60;
         munmap(h, sizeof(shm_hdr_t));
       }
@@ -159,8 +175,8 @@ fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap) {
         shm_hdr_t *h = mmap(NULL, sizeof(shm_hdr_t), PROT_READ, MAP_SHARED, fd, 0);
         int ok = 0;
         if (h != MAP_FAILED) {
-          const unsigned pid = atomic_load_explicit(&h->magic, memory_order_acquire) == SHM_MAGIC ? h->creator : 0;
-          ok = pid && (kill((pid_t)pid, 0) == 0 || errno != ESRCH);
+          const int init = atomic_load_explicit(&h->magic, memory_order_acquire) == SHM_MAGIC;
+          ok = init && h->creator && !creator_dead(h->creator, h->creator_ns);
           munmap(h, sizeof(shm_hdr_t));
         }
         if (ok) break;
@@ -179,6 +195,7 @@ fh_shm_t *fh_shm_open(int rank, int world, const char *name, size_t cap) {
     m->h->world = (unsigned)world;
     m->h->cap = cap;
     m->h->creator = (unsigned)getpid();
+    m->h->creator_ns = pid_ns();
     atomic_store_explicit(&m->h->magic, SHM_MAGIC, memory_order_release);
   } else if (wait_ge_u(&m->h->magic, SHM_MAGIC) != 0 || m->h->world != (unsigned)world || m->h->cap != cap) {
     logmsg(MSG_ERROR, "fscl_amd: shm %s: rank set mismatch", name);

@@ -971,7 +971,10 @@ static void spec_start(void) {
     SP.n_keep = want;
     pthread_cond_broadcast(&SP.cv);
     pthread_mutex_unlock(&SP.mu);
-    for (t = want; t < SP.n_th; t++) pthread_join(SP.th[t], NULL);
+    for (t = want; t < SP.n_th; t++) {
+      pthread_join(SP.th[t], NULL);
+      fh_plan_free(SP.plan + t);  /* the joined worker's plan scratch */
+    }
     SP.n_th = want;
     SP.n_keep = SPEC_MAX;
   }
@@ -989,6 +992,7 @@ static void spec_stop(void) {
   pthread_cond_broadcast(&SP.cv);
   pthread_mutex_unlock(&SP.mu);
   for (t = 0; t < SP.n_th; t++) pthread_join(SP.th[t], NULL);
+  for (t = 0; t <= SPEC_MAX; t++) fh_plan_free(SP.plan + t);  /* workers' and the main thread's plan scratch */
   SP.n_th = 0;
   SP.stop = 0;
   if (!SP.pb_in_pool)

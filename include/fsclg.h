@@ -170,7 +170,11 @@ int fsclg_slot_set_rows_packed(fsclg_ctx *c, int slot, const void *row, int row_
    len + |i - j|)), alone in its group.  ent and grp (n_grp + 1 offsets into ent) are host
    memory the devices read directly (fsclg_host_alloc or fsclg_host_register) and must stay
    unchanged until fsclg_slot_wait(c, slot) returns; only the chr_null values are copied.
-   Every range is checked against n_snps. */
+   Validation is at call time only, on the buffers as they are then: every range is checked
+   against n_snps, and a kind-0 entry's own two ranges for disjointness.  That the entries of one
+   group touch disjoint sites is the CALLER's contract (fh_plan_build guarantees it by
+   construction); entries that overlap across a group race on those sites without an error,
+   though never outside [0, n_snps). */
 typedef struct {
   int32_t i, j, len, kind;
 } fsclg_swap_t;

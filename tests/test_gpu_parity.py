@@ -838,6 +838,21 @@ def test_split_timeout_reruns_unsplit(built, tmp, monkeypatch):
     assert (tmp / "g.txt").read_text() == (GOLD / "g1_p25.out").read_text()
 
 
+def test_split_retry_of_a_bulk_batch(built, tmp, monkeypatch):
+    """The bulk batches (batch >= 2) are split too when they are few cells (FSCL_AMD_BULK_SPLIT,
+    DESIGN.md §5.2), and they may run beside a blocking launch that holds the rest of the device
+    (ADVICE r05): their retry path, forced for the first 3 split bulk launches only
+    (FSCLG_FORCE_SPLIT_RETRY_MINBATCH=2), gives the golden output."""
+    c = manifest()["cases"]["g1_p25"]
+    monkeypatch.setenv("FSCL_AMD_BULK_SPLIT", "4")
+    monkeypatch.setenv("FSCLG_FORCE_SPLIT_RETRY", "3")
+    monkeypatch.setenv("FSCLG_FORCE_SPLIT_RETRY_MINBATCH", "2")
+    fscl_amd.reset_stats()
+    fscl_amd.run(GOLD / c["input"], tmp / "g.txt", **_kw(c["options"]))
+    assert fscl_amd.get_stats()["n_split_retry"] == 3
+    assert (tmp / "g.txt").read_text() == (GOLD / "g1_p25.out").read_text()
+
+
 def test_split_member_late_past_the_wait_is_flagged(built, tmp, monkeypatch):
     """A real timeout, not a forced one: member 0 of cell 0 of every split launch
     sleeps 30 ms before its first arrival (FSCLG_TEST_SPLIT_DELAY_US) while the others wait only
@@ -976,3 +991,29 @@ def test_throughput_mode_two_ranks(built, tmp, tp_case):
         out, err = p.communicate(timeout=600)
         assert p.returncode == 0, err
     assert (tmp / "o0.txt").read_text() == want_out
+
+
+def test_bench_under_torchrun_is_the_drivers_scale_shape(built, tmp):
+    """The driver's SCALE command, at two ranks: `python -m torch.distributed.run --nproc-per-node 2
+    bench.py --gpus 2`, one process per rank.  Both ranks sit on GPU 0 here (FSCL_AMD_DEVICE=0) and
+    torch's own collectives (the segment-name broadcast, the elapsed-time max) run on gloo
+    (FSCL_BENCH_BACKEND); on the driver's 8-GPU node the same path inits nccl with device_id.  C2 at
+    its full size: rc 0, exactly one JSON line (rank 0's), n_gpus 2, and the timed job identical to
+    the oracle's digest of the whole C2 job."""
+    import json
+    env = dict(os.environ, FSCL_BENCH_BACKEND="gloo", FSCL_AMD_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               FSCL_AMD_RANK_TIMEOUT="300")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           f"--master-port={29900 + os.getpid() % 1000}", str(ROOT / "bench.py"), "--gpus", "2", "--config", "C2",
+           "--steps", "1", "--warmup", "0", "--workdir", str(tmp)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 1 and d["value"] > 0
+    assert d["config"]["multi_gpu"].startswith("2 processes"), d["config"]
+    p = d["parity"]
+    assert p["scope"] == "full job" and "C2_bench_p100" in p["fixture"], p
+    assert p["jobs_checked"] == 1 and p["jobs_identical"] == p["jobs_checked"], p
+    assert d["north_star_ratio"]["n_gpus"] == 2 and d["north_star_ratio"]["value"] > 0

@@ -585,4 +585,13 @@ def test_bench_line_assembly_from_recorded_stats(built, monkeypatch):
         assert k in bl, k
     assert bl["anchor"]["source"].startswith("profiles/") and 0.5 < bl["anchor"]["measured_over_extrapolated"] < 2
     line["cpu_baseline"] = bl
+    # the north-star ratio: live from this run's node-linear CPU figure, or the committed one of the workload
+    ns = bench.north_star_ratio(args, 1000, 5.4, 1, bl["node_linear"]["job_s"])
+    assert ns["value"] == bl["node_linear"]["job_s"] / 5.4 and ns["n_gpus"] == 1 and ns["target"] == 100.0
+    ns8 = bench.north_star_ratio(args, 1000, 1.0, 8)
+    tab = _json.loads((ROOT / "profiles" / "cpu_node_linear.json").read_text())["workloads"]["C4/chrall/p1000/parity"]
+    assert ns8["value"] == tab["job_s"] and ns8["n_gpus"] == 8 and (ROOT / tab["source"]).exists()
+    assert ns8["meets_target"] == (tab["job_s"] >= 100.0)
+    assert bench.north_star_ratio(argparse.Namespace(**{**vars(args), "config": "C1"}), 0, 1.0, 1) is None
+    line["north_star_ratio"] = ns
     _json.dumps(line)

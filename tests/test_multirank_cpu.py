@@ -138,6 +138,46 @@ def test_stale_segment_of_a_dead_launch_is_replaced(built, tmp_path):
             os.unlink("/dev/shm" + name)
 
 
+def test_segment_of_another_pid_namespace_counts_as_live(built):
+    """A creator pid means something only in the creator's pid namespace: a segment whose
+    header names a pid that is dead HERE but another namespace is a live job in another container
+    sharing /dev/shm.  Rank 0 must not unlink it (it fails with 'already exists' instead)."""
+    import ctypes as C
+    import struct
+    import fscl_amd
+    L = fscl_amd.get_lib()
+    L.fh_shm_open.restype = C.c_void_p
+    L.fh_shm_open.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_size_t]
+    name = f"/fscl_amd_test_ns_{os.getpid()}"
+    dead_pid = subprocess.run([sys.executable, "-c", "import os; print(os.getpid())"], capture_output=True,
+                              text=True).stdout.strip()
+    ns = os.stat("/proc/self/ns/pid").st_ino
+    # arrive u64, attached u32, magic u32, world u32, creator u32, cap u64, creator_ns u64 (ranks.c shm_hdr_t)
+    hdr = struct.pack("<QIIIIQQ", 0, 0, 0x6673636C, 2, int(dead_pid), 1 << 20, ns + 1)
+    path = "/dev/shm" + name
+    try:
+        with open(path, "wb") as f:
+            f.write(hdr + b"\0" * (4096 * 4 - len(hdr)))
+        assert L.fh_shm_open(0, 2, name.encode(), 1 << 20) is None
+        assert os.path.exists(path)  # left alone
+        # the same header in OUR namespace: the creator is provably gone, the segment is replaced
+        with open(path, "r+b") as f:
+            f.write(struct.pack("<QIIIIQQ", 0, 0, 0x6673636C, 2, int(dead_pid), 1 << 20, ns))
+        env = dict(os.environ, WORLD_SIZE="2", REPO=str(ROOT), SHM_NAME=name, FSCL_AMD_RANK_TIMEOUT="60")
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            script = Path(td) / "s.py"
+            script.write_text(SHM_WORKER)
+            procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r)),
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in (1, 0)]
+            for p in procs:
+                out, err = p.communicate(timeout=300)
+                assert p.returncode == 0, err
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+
+
 def test_device_shares_are_contiguous_and_cover(built):
     """world * n_dev shares (rank r's local device l takes share r * n_dev + l): consecutive,
     disjoint, covering, and each rank's devices form one contiguous range."""
