@@ -108,7 +108,7 @@ static_assert(U_MAIN % 2 == 0 && U_SPLIT % 2 == 0, "the interleaved site array h
 // The site array is interleaved per aligned block of 128 sites (one trip): lane l's 16 bytes
 // hold sites l and l + 64 of the block, so a trip's sites are one dwordx4 per lane (one
 // vector-memory instruction where two dwordx2 cost two: the texture path takes ~16 cycles per
-// wave-instruction whatever its width, tools/vmem_probe).  Site i lives at phys(i).
+// wave-instruction whatever its width, HISTORY.md §10.2, vmem_probe).  Site i lives at phys(i).
 __host__ __device__ __forceinline__ uint32_t phys(uint32_t i) { return (i & ~127u) | ((i & 63u) << 1) | ((i >> 6) & 1u); }
 
 enum { PF_UNSUPPORTED = 1, PF_NOCONV = 2, PF_SPLIT_TIMEOUT = 4 };
@@ -2525,7 +2525,7 @@ __global__ void __launch_bounds__(64) scatter_rows_kernel(uint2* __restrict__ pr
   // One wave per block and no LDS, so that its blocks fit beside two resident search
   // workgroups on a CU (they hold the whole LDS and 6 of the 8 wave slots per SIMD): an LDS-tiled
   // version waited for search workgroups to retire, 137 us per C4 trial at ~7 GB/s, although the
-  // PCIe read itself takes ~30 us (tools/hostread_probe).  A block takes 64 * E
+  // PCIe read itself takes ~30 us (HISTORY.md, hostread_probe).  A block takes 64 * E
   // sites: one 16-B read of the pinned host rows per lane (few, wide PCIe reads), then the wave
   // transposes them by shuffles so that each store k covers 64 consecutive sites.
   constexpr int E = 16 / sizeof(T);
