@@ -132,6 +132,8 @@ struct Params {
   const uint32_t* dband;       // [alpha row][n_iv + 1]: the least |d| with logt(|d|) + lalpha >= thr[j] (band cuts)
   int nd;                      // n_iv + 1 (dband's row stride)
   int band_th;                 // a band's window is staged when its pieces hold at least this many trips
+  int band_nb;                 // at most this many bands (FSCLG_BAND_NB, experiments; NBMAX by default)
+  int band_minp;               // a walk part is cut at a band only where both pieces hold this many trips
   const int32_t* tpos;         // [ceil(n_snps / 128)]: the position of site 128 t (band cut searches)
   const fsclg_cell_t* cells;
   fsclg_point_t* out;
@@ -218,7 +220,9 @@ struct Walk {
 constexpr int NBMAX = FSCLG_NBMAX;
 constexpr int NPIECE = 2 * (NBMAX + 1);  // pieces per walk
 struct BandLds {
-  int16_t cut[MAXWALK][2][NBMAX];
+  alignas(16) int16_t cut[MAXWALK][2][NBMAX];  // -1: the part never reaches the band; -2: dropped (pieces merged)
+  uint32_t dv[MAXWALK][NBMAX];      // the walk's |d| bound of each band (Params::dband)
+  int8_t qof[MAXWALK][2][NBMAX + 1];  // the piece of (walk, part) that group g processes, -1: none
   uint8_t sb[MAXWALK][NPIECE + 1];
   int bbase[NBMAX];
   int nb;
@@ -1094,29 +1098,66 @@ static_assert(MAXWALK <= 32, "band mode: the walk in 5 bits of a tie record");
 // index order with |d| >= D(x).  Right part: q = nb + 1 the remainder, then bands nb - 1 .. 0; a
 // site of band b lies in [cut(b), cut(b - 1)) with cut(x) the FIRST site with |d| >= D(x).
 struct Piece { int part, ta, tb, clo, chi; bool empty; };
+// a walk part's cuts in registers (one 16-byte LDS read); element access by unrolled selects
+static_assert(NBMAX == 8, "a part's cuts are one 16-byte LDS word");
+struct Cuts { int c[NBMAX]; };
 template <class SM>
-__device__ __forceinline__ Piece piece_of(const SM& S, int w, int q, int nb, int ntrL, int ntrR) {
+__device__ __forceinline__ Cuts load_cuts(const SM& S, int w, int part) {
+  const uint4 v = *reinterpret_cast<const uint4*>(&S.bd.cut[w][part][0]);
+  const uint32_t a[4] = {v.x, v.y, v.z, v.w};
+  Cuts k;
+#pragma unroll
+  for (int i = 0; i < 4; i++) { k.c[2 * i] = (int)(int16_t)(a[i] & 0xFFFFu); k.c[2 * i + 1] = (int)(int16_t)(a[i] >> 16); }
+  return k;
+}
+template <class SM>
+__device__ __forceinline__ void store_cuts(SM& S, int w, int part, const Cuts& k) {
+  uint32_t a[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) a[i] = ((uint32_t)k.c[2 * i] & 0xFFFFu) | ((uint32_t)k.c[2 * i + 1] << 16);
+  *reinterpret_cast<uint4*>(&S.bd.cut[w][part][0]) = make_uint4(a[0], a[1], a[2], a[3]);
+}
+__device__ __forceinline__ int cut_at(const Cuts& k, int i) {  // k.c[i], i in [0, NBMAX)
+  int v = -1;
+#pragma unroll
+  for (int j = 0; j < NBMAX; j++) if (j == i) v = k.c[j];
+  return v;
+}
+__device__ __forceinline__ int kept_below(const Cuts& k, int b) {  // the largest j < b with a kept cut, -1
+  int f = -1;
+#pragma unroll
+  for (int j = 0; j < NBMAX; j++) if (j < b && k.c[j] >= 0) f = j;
+  return f;
+}
+// piece q of a walk (site-index order, BandLds) from its part's cuts k: left part (q <= nb): band q,
+// q = nb the remainder, the piece ending (inclusive) at its own kept cut and starting past the
+// nearest kept cut of a higher band; right part: q = nb + 1 the remainder, then bands nb - 1 .. 0,
+// the piece starting at its own kept cut and ending before the nearest kept cut of a higher band
+__device__ __forceinline__ Piece piece_of(const Cuts& k, int q, int nb, int ntrL, int ntrR) {
   Piece pc;
   pc.clo = -1; pc.chi = -1; pc.empty = false;
   if (q <= nb) {
     const int b = q;
     pc.part = 0; pc.ta = 0; pc.tb = ntrL - 1;
-    if (b > 0 && S.bd.cut[w][0][b - 1] >= 0) { pc.ta = S.bd.cut[w][0][b - 1]; pc.clo = b - 1; }
+    const int f = kept_below(k, b);
+    if (f >= 0) { pc.ta = cut_at(k, f); pc.clo = f; }
     if (b < nb) {
-      const int c = S.bd.cut[w][0][b];
+      const int c = cut_at(k, b);
       if (c < 0) pc.empty = true;
       else { pc.tb = c; pc.chi = b; }
     }
+    if (ntrL <= 0) pc.empty = true;
   } else {
     const int b = nb - (q - nb - 1);
     pc.part = 1; pc.ta = 0; pc.tb = ntrR - 1;
-    if (ntrR <= 0) pc.empty = true;
     if (b < nb) {
-      const int c = S.bd.cut[w][1][b];
+      const int c = cut_at(k, b);
       if (c < 0) pc.empty = true;
       else { pc.ta = c; pc.clo = b; }
     }
-    if (b > 0 && S.bd.cut[w][1][b - 1] >= 0) { pc.tb = S.bd.cut[w][1][b - 1]; pc.chi = b - 1; }
+    const int f = kept_below(k, b);
+    if (f >= 0) { pc.tb = cut_at(k, f); pc.chi = f; }
+    if (ntrR <= 0) pc.empty = true;
   }
   return pc;
 }
@@ -1264,22 +1305,51 @@ __device__ __forceinline__ void run_piece_seg(SM& S, int w, int part, int sid, i
       mag += fabs(R);
     }
   };
-  for (int t = 0; t < nt; t++) {
-    const int bs = bs0 + 128 * t;
-    const bool lzlo = t == 0 && dlo != DNONE, lzhi = t == nt - 1 && dhi != DNONE;
-    if (lzlo || lzhi || bs < plo || bs + 127 > phi) trip(bs, t == 0, lzlo, lzhi, std::true_type{});
-    else trip(bs, t == 0, false, false, std::false_type{});
-  }
+  // the masked trips (a lazy cut, or the part's own first / last block) can only be the first and
+  // the last: peeled off, so that the loop body is the unmasked trip alone (a join of both kinds in
+  // the loop makes the waits for the look-ahead load conservative: measured 1.7x per trip)
+  const bool m0 = dlo != DNONE || bs0 < plo || (nt == 1 && (dhi != DNONE || bs0 + 127 > phi));
+  const int bl = bs0 + 128 * (nt - 1);
+  const bool ml = nt > 1 && (dhi != DNONE || bl + 127 > phi);
+  int t = 0;
+  if (m0) { trip(bs0, true, dlo != DNONE, nt == 1 && dhi != DNONE, std::true_type{}); t = 1; }
+  const int tend = ml ? nt - 1 : nt;
+  for (; t < tend; t++) trip(bs0 + 128 * t, t == 0, false, false, std::false_type{});
+  if (ml) trip(bl, false, false, dhi != DNONE, std::true_type{});
   const unsigned long long odd = __ballot(odd_int(sum));
   if (lane == 0 && (__popcll(odd) & 1)) atomicXor(&S.segbits[w][sid >> 5], 1u << (sid & 31));
   acc += sum;
   accm += mag;
 }
 
+// the last t in (lo, hi) whose first position is <= key (STRICT: < key), lo if none (positions
+// ascend over (lo, hi)): an 8-ary search, seven independent probes per dependent round
+template <bool STRICT>
+__device__ __forceinline__ int tpos_search(const int32_t* __restrict__ tpos, int lo, int hi, long long key) {
+  while (hi - lo > 1) {
+    const long long span = hi - lo;
+    int m[7];
+    bool ok[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) m[k] = lo + (int)((span * (k + 1)) >> 3);
+#pragma unroll
+    for (int k = 0; k < 7; k++) { const long long v = tpos[m[k]]; ok[k] = STRICT ? v < key : v <= key; }
+    int nlo = lo, nhi = hi;
+#pragma unroll
+    for (int k = 0; k < 7; k++)
+      if (m[k] > lo && m[k] < hi) {
+        if (ok[k]) nlo = max(nlo, m[k]);
+        else nhi = min(nhi, m[k]);
+      }
+    lo = nlo; hi = nhi;
+  }
+  return lo;
+}
+
 // the |d| bound of band b for walk w (band b's sites: |d| >= it)
 template <class SM>
-__device__ __forceinline__ uint32_t band_d(const SM& S, const Params& P, const Walk& W, int b) {
-  return P.dband[(size_t)W.kd * (size_t)P.nd + (size_t)S.bd.bbase[b]];
+__device__ __forceinline__ uint32_t band_d(const SM& S, int w, int b) {
+  return S.bd.dv[w][b];
 }
 
 // eval_walks in band mode: bounds, the bands and their cuts, the segment numbering, then the
@@ -1322,7 +1392,7 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
     if (lane == 0) {
       int nb = 0;
       if (T >= 0)
-        while (nb < NBMAX) {
+        while (nb < min(P.band_nb, NBMAX)) {
           const int base = T - K * (nb + 1) + 1;
           S.bd.bbase[nb++] = max(base, 0);
           if (base <= 0) break;
@@ -1347,19 +1417,21 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
       const int near = pt.nearest;
       int c = -1;
       if (W.len && (part == 0 || W.nr > 0) && (part ? W.xr : W.xl) >= thrp[S.bd.bbase[b]]) {
-        const long long D = (long long)band_d(S, P, W, b);
+        const uint32_t dvb = P.dband[(size_t)W.kd * (size_t)P.nd + (size_t)S.bd.bbase[b]];
+        S.bd.dv[w][b] = dvb;
+        const long long D = (long long)dvb;
         const long long sw = pt.sweep;
         int t0, lo, hi;
         if (part == 0) {  // the last trip whose first site has pos <= sweep - D
           t0 = (near - W.nl) >> 7;
           lo = t0; hi = (near >> 7) + 1;
           const long long Y = sw - D;
-          while (hi - lo > 1) { const int m = (lo + hi) >> 1; if ((long long)P.tpos[m] <= Y) lo = m; else hi = m; }
+          lo = tpos_search<false>(P.tpos, lo, hi, Y);
         } else {          // the last trip whose first site has pos < sweep + D
           t0 = (near + 1) >> 7;
           lo = t0; hi = ((near + W.nr) >> 7) + 1;
           const long long X = sw + D;
-          while (hi - lo > 1) { const int m = (lo + hi) >> 1; if ((long long)P.tpos[m] < X) lo = m; else hi = m; }
+          lo = tpos_search<true>(P.tpos, lo, hi, X);
         }
         c = lo - t0;
       }
@@ -1367,32 +1439,110 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
     }
   }
   __syncthreads();
-  // segment numbering (a lane per walk) and each group's segments and trips
+  // merging, segment numbering and groups (a lane per walk, the walk's cuts in registers).  A cut is
+  // kept only where the pieces on both sides hold at least band_minp trips (small pieces cost a
+  // segment's fixed work and a masked trip each: 4.8x the segments of the walk-window path with
+  // every cut kept); a merged piece goes to the group of its band with the most trips
   if (wave == 0) {
-    const bool act = lane < nw;
+    const bool act = lane < nw && S.w[lane < nw ? lane : 0].len;
     int ntrL = 0, ntrR = 0;
-    if (act) part_trips(S, lane, ntrL, ntrR);
+    if (lane < nw) part_trips(S, lane, ntrL, ntrR);
+    const int minp = P.band_minp;
+    int8_t qL[NBMAX + 1], qR[NBMAX + 1];  // the piece each group processes, per part
+#pragma unroll
+    for (int g = 0; g <= NBMAX; g++) { qL[g] = -1; qR[g] = -1; }
+    Cuts cl = load_cuts(S, lane < nw ? lane : 0, 0), cr = load_cuts(S, lane < nw ? lane : 0, 1);
+    if (act) {
+      // left part, index order: band 0, 1, ..., nb - 1, the remainder; piece b = (cut[b - 1], cut[b]]
+      int tr[NBMAX + 1];
+      int prev = -1;
+#pragma unroll
+      for (int b = 0; b <= NBMAX; b++) {
+        tr[b] = 0;
+        if (b <= nb) {
+          const int e = b < NBMAX && b < nb ? cl.c[b < NBMAX ? b : 0] : ntrL - 1;
+          if (e >= 0) { tr[b] = e - prev; prev = e; }
+        }
+      }
+      int last = -1, best = nb, btr = -1;
+#pragma unroll
+      for (int b = 0; b <= NBMAX; b++) {
+        if (b <= nb && tr[b] > btr) { btr = tr[b]; best = b; }
+        if (b < nb && b < NBMAX) {
+          const int c = cl.c[b < NBMAX ? b : 0];
+          if (c >= 0) {
+            if (c - last >= minp && ntrL - 1 - c >= minp) {
+#pragma unroll
+              for (int g = 0; g <= NBMAX; g++) if (g == best) qL[g] = (int8_t)b;
+              last = c; best = nb; btr = -1;
+            } else {
+              cl.c[b < NBMAX ? b : 0] = -2;
+            }
+          }
+        } else if (b == nb) {
+#pragma unroll
+          for (int g = 0; g <= NBMAX; g++) if (g == best) qL[g] = (int8_t)nb;
+        }
+      }
+    }
+    if (act && ntrR > 0) {
+      // right part, index order: the remainder, band nb - 1, ..., band 0; piece b = [cut[b], cut[b - 1])
+      int tr[NBMAX];
+      int nxt = ntrR;  // the start of the nearest reached band above
+#pragma unroll
+      for (int b = 0; b < NBMAX; b++) {
+        tr[b] = 0;
+        if (b < nb && cr.c[b] >= 0) { tr[b] = nxt - cr.c[b]; nxt = cr.c[b]; }
+      }
+      int last = 0, low = nb, best = nb, btr = nxt;  // the remainder: [0, lowest reached cut)
+#pragma unroll
+      for (int k = NBMAX - 1; k >= 0; k--) {  // from the bottom band up
+        if (k < nb && cr.c[k] >= 0) {
+          const int c = cr.c[k];
+          if (c - last >= minp && ntrR - c >= minp) {
+#pragma unroll
+            for (int g = 0; g <= NBMAX; g++) if (g == best) qR[g] = (int8_t)(nb + 1 + (nb - low));
+            last = c; low = k; best = k; btr = tr[k];
+          } else {
+            cr.c[k] = -2;
+            if (tr[k] > btr) { btr = tr[k]; best = k; }
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g <= NBMAX; g++) if (g == best) qR[g] = (int8_t)(nb + 1 + (nb - low));
+    }
+    if (lane < nw) {
+      store_cuts(S, lane, 0, cl);
+      store_cuts(S, lane, 1, cr);
+#pragma unroll
+      for (int g = 0; g <= NBMAX; g++) { S.bd.qof[lane][0][g] = qL[g]; S.bd.qof[lane][1][g] = qR[g]; }
+    }
+    // segment ids in site-index order; each group's segments and trips (LDS atomics)
     int run = 0;
     for (int q = 0; q < 2 * (nb + 1); q++) {
-      int nseg = 0, ntr = 0;
-      if (act && S.w[lane].len) {
-        const Piece pc = piece_of(S, lane, q, nb, ntrL, ntrR);
-        if (!pc.empty && pc.tb >= pc.ta) { ntr = pc.tb - pc.ta + 1; nseg = (ntr + TPS - 1) / TPS; }
-      }
-      if (act) S.bd.sb[lane][q] = (uint8_t)run;
-      run += nseg;
-      const int g = q <= nb ? q : nb - (q - nb - 1);
-      int sn = nseg, st = ntr;
+      int nseg = 0;
+      if (act) {
+        const Piece pc = piece_of(q <= nb ? cl : cr, q, nb, ntrL, ntrR);
+        if (!pc.empty && pc.tb >= pc.ta) {
+          nseg = (pc.tb - pc.ta + TPS) / TPS;
+          int g = -1;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) { sn += __shfl_xor(sn, o, 64); st += __shfl_xor(st, o, 64); }
-      if (lane == 0) { S.bd.gitems[g] += sn; S.bd.gtrips[g] += st; }
+          for (int j = 0; j <= NBMAX; j++) if ((q <= nb ? qL[j] : qR[j]) == q) g = j;
+          if (g >= 0) { atomicAdd(&S.bd.gitems[g], nseg); atomicAdd(&S.bd.gtrips[g], pc.tb - pc.ta + 1); }
+        }
+      }
+      if (lane < nw) S.bd.sb[lane][q] = (uint8_t)run;
+      run += nseg;
     }
-    if (act) {
+    if (lane < nw) {
       S.bd.sb[lane][2 * (nb + 1)] = (uint8_t)run;
       S.w[lane].nsl = S.bd.sb[lane][nb + 1];
       S.w[lane].nseg = run;
     }
-    if (lane == 0) {  // runs: a band of at least band_th trips stages its window; the rest ride along
+  }
+  __syncthreads();
+  if (tid == 0) {  // runs: a band of at least band_th trips stages its window; the rest ride along
       int nr = 0;
       for (int g = 0; g <= nb; g++) {
         const bool st = g < nb && S.bd.gtrips[g] >= P.band_th;
@@ -1400,7 +1550,6 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
       }
       S.bd.run_g0[nr] = nb + 1;
       S.bd.nrun = nr;
-    }
   }
   __syncthreads();
   PHASE_MARK(0);
@@ -1420,13 +1569,16 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
       }
       int nit = 0;
       for (int g = g0; g < g1; g++) nit += __builtin_amdgcn_readfirstlane(S.bd.gitems[g]);
+      // each wave takes a contiguous run of the items (consecutive items are mostly one walk's: one
+      // flush per walk, not per item)
       int g = g0, e = 0, ebase = 0;  // entry e = (walk e >> 1, part e & 1) of group g: items from ebase
-      for (int i = wave; i < nit; i += NWAVE) {
+      const int i1 = (nit * (wave + 1)) / NWAVE;
+      for (int i = (nit * wave) / NWAVE; i < i1; i++) {
         int q, cnt;
         for (;;) {
           const int w = e >> 1, part = e & 1;
-          q = part ? nb + 1 + (nb - g) : g;
-          cnt = (int)S.bd.sb[w][q + 1] - (int)S.bd.sb[w][q];
+          q = S.bd.qof[w][part][g];
+          cnt = q >= 0 ? (int)S.bd.sb[w][q + 1] - (int)S.bd.sb[w][q] : 0;
           if (i < ebase + cnt) break;
           ebase += cnt;
           if (++e == 2 * nw) { e = 0; g++; }
@@ -1435,17 +1587,20 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
         const int sid = (int)S.bd.sb[w][q] + s;
         int ntrL, ntrR;
         part_trips(S, w, ntrL, ntrR);
-        const Piece pc = piece_of(S, w, q, nb, ntrL, ntrR);
+        const Piece pc = piece_of(load_cuts(S, w, part), q, nb, ntrL, ntrR);
         const Walk& W = S.w[w];
         const int near = S.pt[W.p].nearest;
         const int ts = pc.ta + s * TPS, nt = min(TPS, pc.tb - ts + 1);
-        const uint32_t dlo = (s == 0 && pc.clo >= 0) ? band_d(S, P, W, pc.clo) : DNONE;
-        const uint32_t dhi = (ts + nt - 1 == pc.tb && pc.chi >= 0) ? band_d(S, P, W, pc.chi) : DNONE;
+        const uint32_t dlo = (s == 0 && pc.clo >= 0) ? band_d(S, w, pc.clo) : DNONE;
+        const uint32_t dhi = (ts + nt - 1 == pc.tb && pc.chi >= 0) ? band_d(S, w, pc.chi) : DNONE;
         const int tp0 = part ? (near + 1) >> 7 : (near - W.nl) >> 7;
         if (w != cw) {
           if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
           cw = w; acc = 0.0; accm = 0.0;
         }
+#ifdef FSCLG_SEGSTATS  // diagnostic: segments in the stats slot 6 (n_ties)
+        if (lane == 0) atomicAdd(&S.cnt[6], 1ull);
+#endif
         run_piece_seg<LDS>(S, w, part, sid, tp0 + ts, nt, dlo, dhi, P, lane, acc, accm);
       }
     }
@@ -1455,7 +1610,9 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
   __syncthreads();
   PHASE_MARK(2);
   if (tid < nw) resolve_walk<SEG, true>(S, tid);
+#ifndef FSCLG_SEGSTATS
   if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;
+#endif
   __syncthreads();
   PHASE_MARK(3);
 #undef PHASE_MARK
@@ -1708,6 +1865,9 @@ __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
         if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
         cw = w; acc = 0.0; accm = 0.0;
       }
+#ifdef FSCLG_SEGSTATS
+      if (lane == 0) atomicAdd(&S.cnt[6], 1ull);
+#endif
       run_segment_idx<LDS, SEGN, SPLIT ? U_SPLIT : U_MAIN>(S, w, g - S.w[w].seg0, g - S.w[w].seg0 + 1, P, lane, acc,
                                                            accm);
       nsg_run++;
@@ -1724,7 +1884,9 @@ __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
   IEV(5, 0, 0);  // combined
   TRACE("  segments done: ties=%d\n", S.n_ties);
   if (tid < nw) resolve_walk<SEGN>(S, tid);
+#ifndef FSCLG_SEGSTATS
   if (tid == 0) S.cnt[6] += (unsigned long long)S.n_ties;
+#endif
   __syncthreads();
   IEV(6, 0, 0);  // resolved
   PHASE_MARK(3);
@@ -3829,8 +3991,18 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.dfail = c->d_dfail;
   P.dband = c->d_dband; P.nd = c->n_iv + 1; P.tpos = c->d_tpos;
   {
-    static const int band_th = getenv("FSCLG_BAND_TH") ? atoi(getenv("FSCLG_BAND_TH")) : -1;  // off until it pays (HISTORY §R6)
+    // band mode where the LDS window is narrow (K <= 6 intervals: the coefficient planes of the
+    // large sample sizes, C5's n = 400 at K = 3), whose planes the vector L1 does not hold; with
+    // planes of a few KB (C2-C4) the walk-window path's global gathers hit L1 and band mode's
+    // layout costs more than it saves (HISTORY §R6.1).  FSCLG_BAND_TH overrides (-1: off); read per
+    // launch, as FSCLG_BAND_NB / FSCLG_BAND_MINP (tests switch them within one process)
+    const int band_env = getenv("FSCLG_BAND_TH") ? atoi(getenv("FSCLG_BAND_TH")) : -2;
+    const int band_th = band_env != -2 ? band_env : (c->c_civ > 0 && c->c_civ <= 6 ? 16 : -1);
     P.band_th = (c->d_dband && c->d_tpos) ? band_th : -1;
+    const int band_nb = getenv("FSCLG_BAND_NB") ? atoi(getenv("FSCLG_BAND_NB")) : NBMAX;
+    P.band_nb = band_nb;
+    const int band_minp = getenv("FSCLG_BAND_MINP") ? atoi(getenv("FSCLG_BAND_MINP")) : 8;
+    P.band_minp = band_minp;
   }
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;

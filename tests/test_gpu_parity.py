@@ -60,6 +60,37 @@ def test_gpu_matches_golden(built, tmp, case):
     assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text()
 
 
+@pytest.mark.parametrize("th,minp,nb", [("0", "1", "8"), ("16", "8", "8"), ("0", "2", "2"), ("0", "1", "0")])
+def test_band_mode_matches_golden(built, tmp, monkeypatch, th, minp, nb):
+    """The band-mode term loop (the phase's walks evaluated interval band by band
+    from LDS windows, pieces cut lazily at |d| thresholds) forced on for every golden case (by
+    default it runs where the LDS window is at most 6 intervals: C5): every window staged with no
+    merging (the most pieces and lazy cuts), the default merging, two bands, and no bands at all;
+    every case's dump and output are the golden ones."""
+    monkeypatch.setenv("FSCLG_BAND_TH", th)
+    monkeypatch.setenv("FSCLG_BAND_MINP", minp)
+    monkeypatch.setenv("FSCLG_BAND_NB", nb)
+    for case in sorted(manifest()["cases"]):
+        c = manifest()["cases"][case]
+        scan = fscl_amd.run(GOLD / c["input"], tmp / "o.txt", **_kw(c["options"]))
+        assert_rows_equal(points_rows(fscl_amd.points(scan)), read_dump(GOLD / f"{case}.dump"), case)
+        assert (tmp / "o.txt").read_text() == (GOLD / f"{case}.out").read_text(), case
+
+
+def test_band_mode_full_size_c4_matches_oracle_fixture(built, tmp, monkeypatch):
+    """Band mode forced on C4's whole 1.0M-SNP genome (45 Mb chromosomes, n = 200, 3 trials), whose
+    default is the walk-window path: the fixture's digest."""
+    monkeypatch.setenv("FSCLG_BAND_TH", "16")
+    sys.path.insert(0, str(GOLD))
+    from make_fullsize import canonical_dump, sha256_file
+    fx = _fullsize()["C4_full_p2"]
+    snp = tmp / "c4.snp"
+    synth.write_snp_file(str(snp), synth.generate(**fx["gen"]))
+    scan = fscl_amd.run(snp, tmp / "g.txt", **_kw(fx["options"]))
+    assert canonical_dump(points_rows(fscl_amd.points(scan))) == fx["dump_sha256"]
+    assert sha256_file(tmp / "g.txt") == fx["out_sha256"]
+
+
 @pytest.mark.parametrize("lookahead", ["0", "2"])
 def test_bisection_lookahead_fallbacks(built, tmp, lookahead):
     """The two-level bisection with the look-ahead off (one level per alpha
@@ -841,10 +872,12 @@ def test_split_timeout_reruns_unsplit(built, tmp, monkeypatch):
 def test_split_retry_of_a_bulk_batch(built, tmp, monkeypatch):
     """The bulk batches (batch >= 2) are split too when they are few cells (FSCL_AMD_BULK_SPLIT,
     DESIGN.md §5.2), and they may run beside a blocking launch that holds the rest of the device
-    (ADVICE r05): their retry path, forced for the first 3 split bulk launches only
+    (ADVICE r05): their retry path, forced for the first 3 split bulk launches only (bulk batches kept
+    apart, FSCL_AMD_NO_MERGE)
     (FSCLG_FORCE_SPLIT_RETRY_MINBATCH=2), gives the golden output."""
     c = manifest()["cases"]["g1_p25"]
     monkeypatch.setenv("FSCL_AMD_BULK_SPLIT", "4")
+    monkeypatch.setenv("FSCL_AMD_NO_MERGE", "1")  # small bulk batches would otherwise join the blocking one
     monkeypatch.setenv("FSCLG_FORCE_SPLIT_RETRY", "3")
     monkeypatch.setenv("FSCLG_FORCE_SPLIT_RETRY_MINBATCH", "2")
     fscl_amd.reset_stats()
