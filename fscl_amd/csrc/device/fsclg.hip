@@ -177,7 +177,6 @@ struct Params {
   int ci_guess;                // the guess for points with no evaluated neighbour (the recent results' mode)
   char* xacc;                  // [n_cells][2] XAcc
   unsigned int* xcnt;          // [n_cells] arrivals; bit 31: some member of the cell timed out (XFAIL_BIT)
-  unsigned int* xtick;         // [n_cells] split cells' segment tickets (zeroed before the launch), or null
   unsigned long long xwait;    // split cells: wall-clock ticks (100 MHz) a member waits for the others
   unsigned long long xdelay;   // tests only (FSCLG_TEST_SPLIT_DELAY_US): member 0 of cell 0 sleeps this
                                // long before its first arrival, so that the other members time out
@@ -273,7 +272,6 @@ struct SmemT {
   int xfail;                      // split cells: PF_SPLIT_TIMEOUT if a member never arrived
   int iev;                        // FSCLG_INST_TRACE: events recorded so far
   int xnt[FSCLG_MAXSPLIT];        // split cells: each member's tie count of the instance
-  int tbase;                      // split cells: the cell's segment tickets before this instance
   typename std::conditional<BAND, BandLds, NoBand>::type bd;
 };
 using Smem = SmemT<MAXWALK, true>;       // the throughput kernel (its LDS window takes the rest)
@@ -1845,35 +1843,7 @@ __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
   // static round-robin of the equal-size segments over the waves; the loop
   // counter lives in an SGPR (a per-lane atomic-dispatch loop here was
   // miscompiled into a loop that never re-issued its atomic)
-  if (SPLIT && P.xtick && P.n_civ == 0) {
-    // split cells, no LDS window: the members' waves take the segments by ticket from the cell's
-    // agent-scope counter (lane 0's fetch-add), in increasing order per wave, so that a member on a
-    // busy CU or dispatched late takes fewer (static dealing left the members waiting on the slowest
-    // one: 17 % of a C4 tail cell at 8 GPUs, HISTORY §R6.3).  Every wave ends on exactly one failed
-    // grab per instance, so the instance consumes seg_total + split * NWAVE tickets on every member
-    const int tot = __builtin_amdgcn_readfirstlane(S.seg_total), base = __builtin_amdgcn_readfirstlane(S.tbase);
-    unsigned int* tk = P.xtick + S.cell;
-    auto grab = [&]() {
-      unsigned int v = 0;
-      if (lane == 0) v = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return (int)__builtin_amdgcn_readfirstlane(v) - base;
-    };
-    int k = 0, cw = -1;
-    double acc = 0.0, accm = 0.0;
-    // (g < 0 only for a member whose control flow left its peers' after a timeout: its cell is re-run)
-    for (int g = grab(); g >= 0 && g < tot; g = grab()) {
-      while (k < nw - 1 && g >= S.w[S.word[k]].seg0 + S.w[S.word[k]].nseg) k++;
-      const int w = S.word[k];
-      if (w != cw) {
-        if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
-        cw = w; acc = 0.0; accm = 0.0;
-      }
-      run_segment_idx<LDS, SEGN, U_SPLIT>(S, w, g - S.w[w].seg0, g - S.w[w].seg0 + 1, P, lane, acc, accm);
-    }
-    if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
-    __syncthreads();  // every wave's grabs are in before the base moves on
-    if (tid == 0) S.tbase = base + tot + P.split * NWAVE;
-  } else {
+  {
     const int ngrp = __builtin_amdgcn_readfirstlane(S.ngrp);
     int k = 0, cw = -1, nsg_run = 0;
     double acc = 0.0, accm = 0.0;
@@ -2149,7 +2119,7 @@ __device__ __forceinline__ void maxpos_body(SM& S, const Params& P) {
   }
   if (tid < 8) S.cnt[tid] = 0;
   if (tid < 5) S.tph[tid] = 0;
-  if (tid == 0) { S.cell = cell; S.member = member; S.inst = 0; S.xfail = 0; S.iev = 0; S.tbase = 0; }
+  if (tid == 0) { S.cell = cell; S.member = member; S.inst = 0; S.xfail = 0; S.iev = 0; }
   if (P.ctrace && tid == 0 && member == 0) { P.ctrace[8 * cell] = wall_clock64(); P.ctrace[8 * cell + 2] = __smid(); }
   if constexpr (LDS) {
     double* thr = reinterpret_cast<double*>(fsclg_dyn + P.off_thr);
@@ -4036,7 +4006,7 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   }
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
-  P.split = 1; P.xacc = nullptr; P.xcnt = nullptr; P.xtick = nullptr;
+  P.split = 1; P.xacc = nullptr; P.xcnt = nullptr;
   {
     const unsigned long long wait_us =
         getenv("FSCLG_SPLIT_WAIT_US") ? strtoull(getenv("FSCLG_SPLIT_WAIT_US"), nullptr, 10) : 1000000ull;
@@ -4332,8 +4302,8 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
       HIPCHK(hipMalloc((void**)&B.d_xacc, xb), "hipMalloc split accumulators");
       B.xacc_cap = xb;
     }
-    if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, 2 * nl))) return r;  // arrivals, then segment tickets
-    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * 2 * nl, B.stream), "hipMemsetAsync");  // the exchange
+    if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, nl))) return r;
+    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");  // the exchange
                                                                                                   // areas need no zeroing
   }
   // the slot's rows and null sums first
@@ -4358,7 +4328,6 @@ static int search_submit_impl(fsclg_ctx* c, int batch, int slot, const fsclg_cel
   }
   if (G > 1) {
     P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
-    P.xtick = getenv("FSCLG_STATIC_DEAL") ? nullptr : B.d_xcnt + nl;
     P.spec_refine = spec_refine_on();
     // latency: no LDS coefficient windows (their loads, repeated by every member for every
     // phase, cost more than the global gathers of a lightly loaded device)
@@ -4513,10 +4482,9 @@ int fsclg_search_points(fsclg_ctx* c, fsclg_point_t* pts, int n_pts) {
       HIPCHK(hipMalloc((void**)&B.d_xacc, xb), "hipMalloc split accumulators");
       B.xacc_cap = xb;
     }
-    if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, 2 * nl))) return r;  // arrivals, then segment tickets
-    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * 2 * nl, B.stream), "hipMemsetAsync");
+    if ((r = ensure_buf(&B.d_xcnt, &B.xcnt_cap, nl))) return r;
+    HIPCHK(hipMemsetAsync(B.d_xcnt, 0, sizeof(unsigned int) * nl, B.stream), "hipMemsetAsync");
     P.split = G; P.xacc = B.d_xacc; P.xcnt = B.d_xcnt;
-    P.xtick = getenv("FSCLG_STATIC_DEAL") ? nullptr : B.d_xcnt + nl;
     P.spec_refine = spec_refine_on();
     P.ivc0 = 0; P.n_civ = 0; P.civ_max = 0; P.n_cache = 0;  // as a split batch: no LDS coefficient windows
     P.off_thr = 0; P.off_nul = (c->n_iv + 1) * 8;
