@@ -135,6 +135,8 @@ struct Params {
   int band_nb;                 // at most this many bands (FSCLG_BAND_NB, experiments; NBMAX by default)
   int band_minp;               // a walk part is cut at a band only where both pieces hold this many trips
   const int32_t* tpos;         // [ceil(n_snps / 128)]: the position of site 128 t (band cut searches)
+  int off_bd;                  // band mode: byte offset of its BandLds in the dynamic LDS (after the logt copy;
+                               // reserved only when band_th >= 0, so the walk-window path keeps the whole window)
   const fsclg_cell_t* cells;
   fsclg_point_t* out;
   unsigned long long* stats;   // 8 counters
@@ -232,7 +234,6 @@ struct BandLds {
   int gitems[NBMAX + 1];            // segments per group
   int gtrips[NBMAX + 1];            // trips per group
 };
-struct NoBand {};
 
 template <int MW, bool BAND = false>
 struct SmemT {
@@ -272,7 +273,6 @@ struct SmemT {
   int xfail;                      // split cells: PF_SPLIT_TIMEOUT if a member never arrived
   int iev;                        // FSCLG_INST_TRACE: events recorded so far
   int xnt[FSCLG_MAXSPLIT];        // split cells: each member's tie count of the instance
-  typename std::conditional<BAND, BandLds, NoBand>::type bd;
 };
 using Smem = SmemT<MAXWALK, true>;       // the throughput kernel (its LDS window takes the rest)
 using SmemSplit = SmemT<MAXWALK_SPLIT>;  // split cells: room for speculative refine walks (no LDS window)
@@ -1101,21 +1101,19 @@ struct Piece { int part, ta, tb, clo, chi; bool empty; };
 // a walk part's cuts in registers (one 16-byte LDS read); element access by unrolled selects
 static_assert(NBMAX == 8, "a part's cuts are one 16-byte LDS word");
 struct Cuts { int c[NBMAX]; };
-template <class SM>
-__device__ __forceinline__ Cuts load_cuts(const SM& S, int w, int part) {
-  const uint4 v = *reinterpret_cast<const uint4*>(&S.bd.cut[w][part][0]);
+__device__ __forceinline__ Cuts load_cuts(const BandLds& bd, int w, int part) {
+  const uint4 v = *reinterpret_cast<const uint4*>(&bd.cut[w][part][0]);
   const uint32_t a[4] = {v.x, v.y, v.z, v.w};
   Cuts k;
 #pragma unroll
   for (int i = 0; i < 4; i++) { k.c[2 * i] = (int)(int16_t)(a[i] & 0xFFFFu); k.c[2 * i + 1] = (int)(int16_t)(a[i] >> 16); }
   return k;
 }
-template <class SM>
-__device__ __forceinline__ void store_cuts(SM& S, int w, int part, const Cuts& k) {
+__device__ __forceinline__ void store_cuts(BandLds& bd, int w, int part, const Cuts& k) {
   uint32_t a[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) a[i] = ((uint32_t)k.c[2 * i] & 0xFFFFu) | ((uint32_t)k.c[2 * i + 1] << 16);
-  *reinterpret_cast<uint4*>(&S.bd.cut[w][part][0]) = make_uint4(a[0], a[1], a[2], a[3]);
+  *reinterpret_cast<uint4*>(&bd.cut[w][part][0]) = make_uint4(a[0], a[1], a[2], a[3]);
 }
 __device__ __forceinline__ int cut_at(const Cuts& k, int i) {  // k.c[i], i in [0, NBMAX)
   int v = -1;
@@ -1347,9 +1345,8 @@ __device__ __forceinline__ int tpos_search(const int32_t* __restrict__ tpos, int
 }
 
 // the |d| bound of band b for walk w (band b's sites: |d| >= it)
-template <class SM>
-__device__ __forceinline__ uint32_t band_d(const SM& S, int w, int b) {
-  return S.bd.dv[w][b];
+__device__ __forceinline__ uint32_t band_d(const BandLds& bd, int w, int b) {
+  return bd.dv[w][b];
 }
 
 // eval_walks in band mode: bounds, the bands and their cuts, the segment numbering, then the
@@ -1357,6 +1354,7 @@ __device__ __forceinline__ uint32_t band_d(const SM& S, int w, int b) {
 // pieces are too few to pay for their own), the remainder last; resolve as eval_walks.
 template <bool LDS, class SM>
 __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
+  BandLds& bd = *reinterpret_cast<BandLds*>(fsclg_dyn + P.off_bd);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nw = __builtin_amdgcn_readfirstlane(S.nwalk);
 #ifdef FSCLG_PHASE_TIMING
@@ -1371,7 +1369,7 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
     S.P[tid] = 0; S.Q[tid] = 0; S.Pd[tid] = 0.0; S.Qd[tid] = 0.0; S.wflag[tid] = 0; S.need_slow[tid] = 0;
     for (int j = 0; j < SEGWORDS; j++) S.segbits[tid][j] = 0;
   }
-  if (tid <= NBMAX) { S.bd.gitems[tid] = 0; S.bd.gtrips[tid] = 0; }
+  if (tid <= NBMAX) { bd.gitems[tid] = 0; bd.gtrips[tid] = 0; }
   if (tid == 0) S.n_ties = 0;
   __syncthreads();
   // the bands: K-interval windows from the phase's top interval T downwards (wave 0, a lane per walk)
@@ -1394,16 +1392,16 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
       if (T >= 0)
         while (nb < min(P.band_nb, NBMAX)) {
           const int base = T - K * (nb + 1) + 1;
-          S.bd.bbase[nb++] = max(base, 0);
+          bd.bbase[nb++] = max(base, 0);
           if (base <= 0) break;
         }
-      S.bd.nb = nb;
+      bd.nb = nb;
       S.cnt[0] += (unsigned long long)terms;
       S.cnt[2] += nw;
     }
   }
   __syncthreads();
-  const int nb = __builtin_amdgcn_readfirstlane(S.bd.nb);
+  const int nb = __builtin_amdgcn_readfirstlane(bd.nb);
   // the cuts (a thread per walk, part, band): the trip holding the part's first site in walk order
   // whose |d| reaches the band, by bisection over the trips' first positions (sorted within the
   // part; the part's first trip counts as at or before the cut); -1 if the part's farthest site
@@ -1416,9 +1414,9 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
       const Pt& pt = S.pt[W.p];
       const int near = pt.nearest;
       int c = -1;
-      if (W.len && (part == 0 || W.nr > 0) && (part ? W.xr : W.xl) >= thrp[S.bd.bbase[b]]) {
-        const uint32_t dvb = P.dband[(size_t)W.kd * (size_t)P.nd + (size_t)S.bd.bbase[b]];
-        S.bd.dv[w][b] = dvb;
+      if (W.len && (part == 0 || W.nr > 0) && (part ? W.xr : W.xl) >= thrp[bd.bbase[b]]) {
+        const uint32_t dvb = P.dband[(size_t)W.kd * (size_t)P.nd + (size_t)bd.bbase[b]];
+        bd.dv[w][b] = dvb;
         const long long D = (long long)dvb;
         const long long sw = pt.sweep;
         int t0, lo, hi;
@@ -1435,7 +1433,7 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
         }
         c = lo - t0;
       }
-      S.bd.cut[w][part][b] = (int16_t)c;
+      bd.cut[w][part][b] = (int16_t)c;
     }
   }
   __syncthreads();
@@ -1451,7 +1449,7 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
     int8_t qL[NBMAX + 1], qR[NBMAX + 1];  // the piece each group processes, per part
 #pragma unroll
     for (int g = 0; g <= NBMAX; g++) { qL[g] = -1; qR[g] = -1; }
-    Cuts cl = load_cuts(S, lane < nw ? lane : 0, 0), cr = load_cuts(S, lane < nw ? lane : 0, 1);
+    Cuts cl = load_cuts(bd, lane < nw ? lane : 0, 0), cr = load_cuts(bd, lane < nw ? lane : 0, 1);
     if (act) {
       // left part, index order: band 0, 1, ..., nb - 1, the remainder; piece b = (cut[b - 1], cut[b]]
       int tr[NBMAX + 1];
@@ -1513,10 +1511,10 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
       for (int g = 0; g <= NBMAX; g++) if (g == best) qR[g] = (int8_t)(nb + 1 + (nb - low));
     }
     if (lane < nw) {
-      store_cuts(S, lane, 0, cl);
-      store_cuts(S, lane, 1, cr);
+      store_cuts(bd, lane, 0, cl);
+      store_cuts(bd, lane, 1, cr);
 #pragma unroll
-      for (int g = 0; g <= NBMAX; g++) { S.bd.qof[lane][0][g] = qL[g]; S.bd.qof[lane][1][g] = qR[g]; }
+      for (int g = 0; g <= NBMAX; g++) { bd.qof[lane][0][g] = qL[g]; bd.qof[lane][1][g] = qR[g]; }
     }
     // segment ids in site-index order; each group's segments and trips (LDS atomics)
     int run = 0;
@@ -1529,15 +1527,15 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
           int g = -1;
 #pragma unroll
           for (int j = 0; j <= NBMAX; j++) if ((q <= nb ? qL[j] : qR[j]) == q) g = j;
-          if (g >= 0) { atomicAdd(&S.bd.gitems[g], nseg); atomicAdd(&S.bd.gtrips[g], pc.tb - pc.ta + 1); }
+          if (g >= 0) { atomicAdd(&bd.gitems[g], nseg); atomicAdd(&bd.gtrips[g], pc.tb - pc.ta + 1); }
         }
       }
-      if (lane < nw) S.bd.sb[lane][q] = (uint8_t)run;
+      if (lane < nw) bd.sb[lane][q] = (uint8_t)run;
       run += nseg;
     }
     if (lane < nw) {
-      S.bd.sb[lane][2 * (nb + 1)] = (uint8_t)run;
-      S.w[lane].nsl = S.bd.sb[lane][nb + 1];
+      bd.sb[lane][2 * (nb + 1)] = (uint8_t)run;
+      S.w[lane].nsl = bd.sb[lane][nb + 1];
       S.w[lane].nseg = run;
     }
   }
@@ -1545,22 +1543,22 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
   if (tid == 0) {  // runs: a band of at least band_th trips stages its window; the rest ride along
       int nr = 0;
       for (int g = 0; g <= nb; g++) {
-        const bool st = g < nb && S.bd.gtrips[g] >= P.band_th;
-        if (st || nr == 0) { S.bd.run_g0[nr] = g; S.bd.run_stage[nr] = st ? 1 : 0; nr++; }
+        const bool st = g < nb && bd.gtrips[g] >= P.band_th;
+        if (st || nr == 0) { bd.run_g0[nr] = g; bd.run_stage[nr] = st ? 1 : 0; nr++; }
       }
-      S.bd.run_g0[nr] = nb + 1;
-      S.bd.nrun = nr;
+      bd.run_g0[nr] = nb + 1;
+      bd.nrun = nr;
   }
   __syncthreads();
   PHASE_MARK(0);
   {
     int cw = -1;
     double acc = 0.0, accm = 0.0;
-    const int nrun = __builtin_amdgcn_readfirstlane(S.bd.nrun);
+    const int nrun = __builtin_amdgcn_readfirstlane(bd.nrun);
     for (int r = 0; r < nrun; r++) {
-      const int g0 = __builtin_amdgcn_readfirstlane(S.bd.run_g0[r]), g1 = __builtin_amdgcn_readfirstlane(S.bd.run_g0[r + 1]);
-      if (__builtin_amdgcn_readfirstlane(S.bd.run_stage[r])) {
-        const int wb = __builtin_amdgcn_readfirstlane(S.bd.bbase[g0]);
+      const int g0 = __builtin_amdgcn_readfirstlane(bd.run_g0[r]), g1 = __builtin_amdgcn_readfirstlane(bd.run_g0[r + 1]);
+      if (__builtin_amdgcn_readfirstlane(bd.run_stage[r])) {
+        const int wb = __builtin_amdgcn_readfirstlane(bd.bbase[g0]);
         if (wb != __builtin_amdgcn_readfirstlane(S.ivc0)) {  // uniform over the workgroup
           __syncthreads();
           load_window(S, P, wb);
@@ -1568,7 +1566,7 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
         }
       }
       int nit = 0;
-      for (int g = g0; g < g1; g++) nit += __builtin_amdgcn_readfirstlane(S.bd.gitems[g]);
+      for (int g = g0; g < g1; g++) nit += __builtin_amdgcn_readfirstlane(bd.gitems[g]);
       // each wave takes a contiguous run of the items (consecutive items are mostly one walk's: one
       // flush per walk, not per item)
       int g = g0, e = 0, ebase = 0;  // entry e = (walk e >> 1, part e & 1) of group g: items from ebase
@@ -1577,22 +1575,22 @@ __device__ __forceinline__ void eval_walks_band(SM& S, const Params& P) {
         int q, cnt;
         for (;;) {
           const int w = e >> 1, part = e & 1;
-          q = S.bd.qof[w][part][g];
-          cnt = q >= 0 ? (int)S.bd.sb[w][q + 1] - (int)S.bd.sb[w][q] : 0;
+          q = bd.qof[w][part][g];
+          cnt = q >= 0 ? (int)bd.sb[w][q + 1] - (int)bd.sb[w][q] : 0;
           if (i < ebase + cnt) break;
           ebase += cnt;
           if (++e == 2 * nw) { e = 0; g++; }
         }
         const int w = e >> 1, part = e & 1, s = i - ebase;
-        const int sid = (int)S.bd.sb[w][q] + s;
+        const int sid = (int)bd.sb[w][q] + s;
         int ntrL, ntrR;
         part_trips(S, w, ntrL, ntrR);
-        const Piece pc = piece_of(load_cuts(S, w, part), q, nb, ntrL, ntrR);
+        const Piece pc = piece_of(load_cuts(bd, w, part), q, nb, ntrL, ntrR);
         const Walk& W = S.w[w];
         const int near = S.pt[W.p].nearest;
         const int ts = pc.ta + s * TPS, nt = min(TPS, pc.tb - ts + 1);
-        const uint32_t dlo = (s == 0 && pc.clo >= 0) ? band_d(S, w, pc.clo) : DNONE;
-        const uint32_t dhi = (ts + nt - 1 == pc.tb && pc.chi >= 0) ? band_d(S, w, pc.chi) : DNONE;
+        const uint32_t dlo = (s == 0 && pc.clo >= 0) ? band_d(bd, w, pc.clo) : DNONE;
+        const uint32_t dhi = (ts + nt - 1 == pc.tb && pc.chi >= 0) ? band_d(bd, w, pc.chi) : DNONE;
         const int tp0 = part ? (near + 1) >> 7 : (near - W.nl) >> 7;
         if (w != cw) {
           if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
@@ -2905,6 +2903,8 @@ struct fsclg_ctx {
   int ivhist_n = 0;
   int c_ivc0 = 0, c_civ = 0, c_crow = 0;
   double c_cover = 0.0;
+  int c_ivc0_b = 0, c_civ_b = 0;         // the window beside band mode's BandLds (Params::off_bd)
+  double c_cover_b = 0.0;
   // alpha grid
   std::vector<double> h_coarse, h_refine;
   std::vector<int32_t> h_nref;
@@ -3902,8 +3902,10 @@ static int slot_windows_impl(fsclg_ctx* c, int slot, const fsclg_cell_t* cells, 
 // Every row is held: a miss sends the whole wave's gather to the global table, so a row
 // prefix (a per-lane miss rate) would miss in nearly every wave, while an interval window
 // misses in whole waves (neighbouring sites have nearly equal log distance).
+constexpr int BAND_LDS_BYTES = (int)((sizeof(BandLds) + 15) / 16 * 16);
 static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
   c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
+  c->c_ivc0_b = 0; c->c_civ_b = 0; c->c_cover_b = 0.0;
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0) -
                    (c->lx_on && FSCLG_LOG_CALC >= 2 ? LX_BYTES + 16 : 0);
@@ -3926,6 +3928,9 @@ static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
   int bj;
   c->c_cover = best_iv(K, bj);
   c->c_ivc0 = bj; c->c_civ = K; c->c_crow = R;
+  // band mode's window: the same choice in the room its BandLds leaves (16 B aligned after the rest)
+  const int Kb = std::min(c->n_iv, (room - BAND_LDS_BYTES - 16) / (R * 32));
+  if (Kb > 0) { c->c_cover_b = best_iv(Kb, bj); c->c_ivc0_b = bj; c->c_civ_b = Kb; }
 }
 
 // Choose the LDS coefficient window: intervals [ivc0, ivc0 + K) x every device row, K * rows
@@ -3936,6 +3941,7 @@ static void choose_window(fsclg_ctx* c, const std::vector<double>& hist) {
 static void plan_cache(fsclg_ctx* c) {
   c->plan_dirty = false;
   c->c_ivc0 = 0; c->c_civ = 0; c->c_crow = 0; c->c_cover = 0.0;
+  c->c_ivc0_b = 0; c->c_civ_b = 0; c->c_cover_b = 0.0;
   if (getenv("FSCLG_NO_WINDOW")) return;  // experiment: every coefficient from the global table
   const int stat = (int)((sizeof(Smem) + 15) / 16 * 16);
   const int room = LDS_WG - stat - (c->n_iv + 1) * 8 - (c->n_rows + 1) * 8 - (c->lt_hi ? (c->lt_hi - 256) * 8 : 0) -
@@ -3971,6 +3977,9 @@ static void plan_cache(fsclg_ctx* c) {
 #endif
 }
 
+// band mode by default where its window is narrow (K <= 6 intervals, C5); -1: the walk-window path
+static int band_default(const fsclg_ctx* c) { return c->c_civ_b > 0 && c->c_civ_b <= 6 ? 16 : -1; }
+
 static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int eval_range, int bp_resl) {
   const Slot& S = c->slot[slot];
   Params P;
@@ -3979,31 +3988,35 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   P.inv_step = 1.0 / c->step; P.iv_off = -LOG_AD_MIN * P.inv_step - 1e-9;
   // dynamic LDS: the planned coefficient window, thresholds and null rows
   if (c->plan_dirty) plan_cache(c);
-  P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; P.civ_max = std::max(c->c_civ - 1, 0);
+  {
+    // band mode where the LDS window is narrow (K <= 6 intervals: the coefficient planes of the
+    // large sample sizes, C5's n = 400 at K = 3), whose planes the vector L1 does not hold; with
+    // planes of a few KB (C2-C4) the walk-window path's global gathers hit L1 and band mode's
+    // layout costs more than it saves (HISTORY §R6.1).  FSCLG_BAND_TH overrides (-1: off); read per
+    // launch, as FSCLG_BAND_NB / FSCLG_BAND_MINP (tests switch them within one process).  Band
+    // mode's BandLds sits in the dynamic LDS after the logt copy, so its window is c_civ_b
+    const int band_env = getenv("FSCLG_BAND_TH") ? atoi(getenv("FSCLG_BAND_TH")) : -2;
+    const int band_th = band_env != -2 ? band_env : band_default(c);
+    P.band_th = (c->d_dband && c->d_tpos && c->c_civ_b > 0) ? band_th : -1;
+    const int band_nb = getenv("FSCLG_BAND_NB") ? atoi(getenv("FSCLG_BAND_NB")) : NBMAX;
+    P.band_nb = band_nb;
+    const int band_minp = getenv("FSCLG_BAND_MINP") ? atoi(getenv("FSCLG_BAND_MINP")) : 8;
+    P.band_minp = band_minp;
+  }
+  if (P.band_th >= 0) { P.ivc0 = c->c_ivc0_b; P.n_civ = c->c_civ_b; }
+  else { P.ivc0 = c->c_ivc0; P.n_civ = c->c_civ; }
+  P.civ_max = std::max(P.n_civ - 1, 0);
   P.n_cache = P.n_civ * P.stride;
   P.off_thr = P.n_cache * 32; P.off_nul = P.off_thr + (c->n_iv + 1) * 8;
   P.off_lt = P.off_nul + (c->n_rows + 1) * 8 - 256 * 8; P.lt_hi = c->lt_hi;  // entry i at off_lt + 8 i
   P.lt_span = c->lt_hi > 256 ? ((uint32_t)c->lt_hi << 16) - 0x1000000u : 0u;  // lt_hi <= 32768
   P.lx = c->d_lx; P.lx_on = FSCLG_LOG_CALC >= 2 ? c->lx_on : 0;  // FSCLG_LOG_CALC=1: set for split launches
   P.off_lx = (P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0) + 15) & ~15;
+  P.off_bd = ((P.lx_on ? P.off_lx + LX_BYTES : P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0)) + 15) & ~15;
   P.chr_start = c->d_chr_start; P.chr_n = c->d_chr_n; P.chr_null = S.d_chr_null; P.win_null = S.d_win_null;
   P.la_coarse = c->d_la_coarse; P.la_refine = c->d_la_refine; P.n_refine = c->d_n_refine;
   P.dfail = c->d_dfail;
   P.dband = c->d_dband; P.nd = c->n_iv + 1; P.tpos = c->d_tpos;
-  {
-    // band mode where the LDS window is narrow (K <= 6 intervals: the coefficient planes of the
-    // large sample sizes, C5's n = 400 at K = 3), whose planes the vector L1 does not hold; with
-    // planes of a few KB (C2-C4) the walk-window path's global gathers hit L1 and band mode's
-    // layout costs more than it saves (HISTORY §R6.1).  FSCLG_BAND_TH overrides (-1: off); read per
-    // launch, as FSCLG_BAND_NB / FSCLG_BAND_MINP (tests switch them within one process)
-    const int band_env = getenv("FSCLG_BAND_TH") ? atoi(getenv("FSCLG_BAND_TH")) : -2;
-    const int band_th = band_env != -2 ? band_env : (c->c_civ > 0 && c->c_civ <= 6 ? 16 : -1);
-    P.band_th = (c->d_dband && c->d_tpos) ? band_th : -1;
-    const int band_nb = getenv("FSCLG_BAND_NB") ? atoi(getenv("FSCLG_BAND_NB")) : NBMAX;
-    P.band_nb = band_nb;
-    const int band_minp = getenv("FSCLG_BAND_MINP") ? atoi(getenv("FSCLG_BAND_MINP")) : 8;
-    P.band_minp = band_minp;
-  }
   P.cells = B.p_cells; P.out = B.p_out; P.stats = c->d_stats; P.ctrace = nullptr; P.ivhist = nullptr;
   P.epos = nullptr; P.n_ep = 0; P.ept = nullptr; P.cell_ep = nullptr;
   P.split = 1; P.xacc = nullptr; P.xcnt = nullptr;
@@ -4064,7 +4077,9 @@ static int launch_blocks(hipStream_t stream, const Params& P, int n) {
 }
 static int launch_blocks_impl(hipStream_t stream, const Params& P, int n) {
   const int grid = n;
-  const int dyn = P.lx_on ? P.off_lx + LX_BYTES : P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0);
+  const int dyn = (P.band_th >= 0 && P.n_civ > 0 && P.split <= 1)
+                      ? P.off_bd + BAND_LDS_BYTES
+                      : (P.lx_on ? P.off_lx + LX_BYTES : P.off_lt + 256 * 8 + (P.lt_hi ? (P.lt_hi - 256) * 8 : 0));
   const int stat_m = (int)((sizeof(Smem) + 15) / 16 * 16), stat_s = (int)((sizeof(SmemSplit) + 15) / 16 * 16);
   if ((P.split > 1 ? stat_s : stat_m) + dyn <= LDS_WG) {
     static unsigned long long attr_set = 0;  // per device (bit = device id)
@@ -4556,7 +4571,9 @@ int fsclg_get_stats(fsclg_ctx* c, fsclg_stats_t* st) {
     st->busy_ms = busy;
   }
   if (c->plan_dirty) plan_cache(c);
-  st->cache_iv0 = c->c_ivc0; st->cache_n_iv = c->c_civ; st->cache_n_rows = c->c_crow; st->cache_cover = c->c_cover;
+  if (band_default(c) >= 0) { st->cache_iv0 = c->c_ivc0_b; st->cache_n_iv = c->c_civ_b; st->cache_cover = c->c_cover_b; }
+  else { st->cache_iv0 = c->c_ivc0; st->cache_n_iv = c->c_civ; st->cache_cover = c->c_cover; }
+  st->cache_n_rows = c->c_crow;
   return FSCLG_OK;
 }
 
