@@ -438,7 +438,11 @@ def bench_line(args, cfg: dict, st: dict, units: float, elapsed: float, n_gpus: 
             traffic = None
     mem = None
     mem_path = ROOT / "profiles" / "r03b_pmc_mem_c4_c2.json"
-    if mem_path.exists() and args.config.lower() in ("c4", "c2") and not args.chromosomes:
+    if prof and prof.get("memory_path", {}).get("per_term"):  # the same profile's mem / tcc passes
+        m = prof["memory_path"]
+        mem = {"source": prof_src, **{k: round(v, 3) for k, v in m["per_term"].items()},
+               "tcc_hit_rate": m.get("tcc_hit_rate"), "hbm_fetch_bytes_per_term": m.get("hbm_fetch_bytes_per_term")}
+    elif mem_path.exists() and args.config.lower() in ("c4", "c2") and not args.chromosomes:
         m = json.loads(mem_path.read_text())[args.config.lower()]
         t = m["totals_over_job"]
         mem = {"source": str(mem_path.relative_to(ROOT)), **{k: round(v, 3) for k, v in m["per_term"].items()},

@@ -262,6 +262,7 @@ struct SmemT {
   int ngrp;                       // walk groups of the phase (one LDS window each), in segment order
   int gwb[MW];
   int gseg[MW + 1];
+  int gk[MW + 1];                 // the group's walks: word[gk[g] .. gk[g + 1])
   int word[MW];              // walks in segment order
   int hkey;                       // interval-histogram key of the phase: 0 coarse, 1 + c refine around coarse c
   int hitmask;                    // split cells: the points whose speculative refine walks were the right ones
@@ -274,7 +275,10 @@ struct SmemT {
   int iev;                        // FSCLG_INST_TRACE: events recorded so far
   int xnt[FSCLG_MAXSPLIT];        // split cells: each member's tie count of the instance
 };
-using Smem = SmemT<MAXWALK, true>;       // the throughput kernel (its LDS window takes the rest)
+using Smem = SmemT<MAXWALK>;             // the throughput kernel (its LDS window takes the rest)
+using SmemBand = SmemT<MAXWALK, true>;   // the same in band mode: a kernel of its own, so that band mode's
+                                         // layout code does not raise the walk-window kernel's registers
+static_assert(sizeof(Smem) == sizeof(SmemBand), "band mode's LDS block is dynamic (Params::off_bd)");
 using SmemSplit = SmemT<MAXWALK_SPLIT>;  // split cells: room for speculative refine walks (no LDS window)
 
 
@@ -673,6 +677,20 @@ __device__ __forceinline__ double walk_sequential(const SM& S, const Walk& W, co
   return acc;
 }
 
+// FSCLG_SITE_MAJOR (default): a walk's left part is cut on the grid that ENDS at the block holding the
+// nearest site (the right part's grid starts at the block after it), so that both grids are the same
+// for every walk of a point, and the waves are dealt a phase's segments site-major: slice (j, part) is
+// the j-th segment from the nearest site of every walk that reaches it, so the waves working at once
+// read the same sites and log-table entries for different alphas (logt(|d|) does not depend on alpha)
+// and those reads hit the vector L1.  0: the left grid from the walk's far end, walk-major dealing.
+#ifndef FSCLG_SITE_MAJOR
+#define FSCLG_SITE_MAJOR 1
+#endif
+#ifndef FSCLG_LEFT_ANCHOR
+#define FSCLG_LEFT_ANCHOR FSCLG_SITE_MAJOR
+#endif
+__device__ __forceinline__ int left_anchor(int near) { return (near & ~127) + 128; }
+
 // A walk covers the site indices [nearest - nl, nearest + nr]; its left part
 // [nearest - nl, nearest] (walked downwards, sm-search.c:122-128) and right part
 // [nearest + 1, nearest + nr] are cut into separate segments (left ones first), so each
@@ -683,8 +701,13 @@ template <int SEGN>
 __device__ __forceinline__ void seg_bounds(const Walk& W, const Pt& pt, int s, int& ib, int& ie) {
   const int lo = pt.nearest - W.nl, near = pt.nearest, hi = pt.nearest + W.nr;
   if (s < W.nsl) {
+#if FSCLG_LEFT_ANCHOR
+    const int A = left_anchor(near), j = W.nsl - 1 - s;
+    ib = max(lo, A - (j + 1) * SEGN); ie = min(A - j * SEGN, near + 1);
+#else
     const int b0 = lo & ~127;
     ib = max(lo, b0 + s * SEGN); ie = min(b0 + (s + 1) * SEGN, near + 1);
+#endif
   } else {
     const int b1 = (near + 1) & ~127, t = s - W.nsl;
     ib = max(near + 1, b1 + t * SEGN); ie = min(b1 + (t + 1) * SEGN, hi + 1);
@@ -694,15 +717,25 @@ __device__ __forceinline__ void seg_bounds(const Walk& W, const Pt& pt, int s, i
 // segments of a walk's two parts (layout)
 template <int SEGN>
 __device__ __forceinline__ void seg_counts(int lo, int near, int hi, int& nsl, int& nsr) {
+#if FSCLG_LEFT_ANCHOR
+  nsl = (left_anchor(near) - (lo & ~127) + SEGN - 1) / SEGN;
+#else
   nsl = (near - (lo & ~127)) / SEGN + 1;
+#endif
   nsr = hi > near ? (hi - ((near + 1) & ~127)) / SEGN + 1 : 0;
 }
+
 
 // the segment of site index i of the walk
 template <int SEGN>
 __device__ __forceinline__ int seg_of(const Walk& W, const Pt& pt, int i) {
   const int lo = pt.nearest - W.nl, near = pt.nearest;
+#if FSCLG_LEFT_ANCHOR
+  (void)lo;
+  return i <= near ? W.nsl - 1 - (left_anchor(near) - 1 - i) / SEGN : W.nsl + (i - ((near + 1) & ~127)) / SEGN;
+#else
   return i <= near ? (i - (lo & ~127)) / SEGN : W.nsl + (i - ((near + 1) & ~127)) / SEGN;
+#endif
 }
 
 __device__ __forceinline__ bool odd_int(double v) { return v - 2.0 * floor(0.5 * v) != 0.0; }
@@ -1817,7 +1850,7 @@ __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
       const int wbk = __builtin_amdgcn_readlane(wb, l), lenk = __builtin_amdgcn_readlane(len, l),
                 s0k = __builtin_amdgcn_readlane(seg0, l);
       if (lenk && (ng == 0 || wbk < gprev - 2)) {
-        if (lane == 0) { S.gwb[ng] = wbk; S.gseg[ng] = s0k; }
+        if (lane == 0) { S.gwb[ng] = wbk; S.gseg[ng] = s0k; S.gk[ng] = k; }
         ng++;
         gprev = wbk;
       }
@@ -1828,6 +1861,7 @@ __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
     for (int o = 32; o > 0; o >>= 1) { tot += __shfl_xor(tot, o, 64); terms += __shfl_xor(terms, o, 64); }
     if (lane == 0) {
       S.gseg[ng] = tot;
+      S.gk[ng] = nw;
       S.ngrp = ng;
       S.seg_total = tot;
       S.cnt[0] += (unsigned long long)terms;
@@ -1856,18 +1890,43 @@ __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
      // split cells: the members deal the segments round-robin
      const int mstride = SPLIT ? NWAVE * P.split : NWAVE;
      const int g0 = SPLIT ? __builtin_amdgcn_readfirstlane(S.member) * NWAVE + wave : wave;
+#if FSCLG_SITE_MAJOR
+     // site-major: the group's ids run over the slices (j, part) = (0, left), (0, right), (1, left), ...;
+     // slice (j, part) holds, in walk order, the walks whose part has more than j segments (lane l of
+     // every wave holds the group's l-th walk and its part counts); id -> (walk, segment) by a ballot
+     const int k0 = __builtin_amdgcn_readfirstlane(S.gk[gi]), nwg = __builtin_amdgcn_readfirstlane(S.gk[gi + 1]) - k0;
+     int wl = 0, nsl_l = 0, nsr_l = 0;
+     if (lane < nwg) { wl = S.word[k0 + lane]; nsl_l = S.w[wl].nsl; nsr_l = S.w[wl].nseg - nsl_l; }
+     int base = __builtin_amdgcn_readfirstlane(S.gseg[gi]), sj = 0, spart = 0;
+     unsigned long long M = __ballot(lane < nwg && nsl_l > 0);
+     (void)k;
+#endif
      for (int g = __builtin_amdgcn_readfirstlane(S.gseg[gi]) + g0; g < ge; g += mstride) {
+#if FSCLG_SITE_MAJOR
+      while (g >= base + (int)__popcll(M) && sj < MAXSEG_W) {  // g < ge: a later slice holds it
+        base += (int)__popcll(M);
+        if (spart == 0) spart = 1; else { spart = 0; sj++; }
+        M = __ballot(lane < nwg && (spart ? nsr_l : nsl_l) > sj);
+      }
+      if (g >= base + (int)__popcll(M)) break;  // never: the slices hold exactly the group's segments
+      const int rk = g - base;  // the rk-th walk of the slice
+      const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(M >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)M, 0u));
+      const int l = __ffsll(__ballot(((M >> lane) & 1ull) && below == rk)) - 1;
+      const int w = __builtin_amdgcn_readlane(wl, l);
+      const int sg = spart ? __builtin_amdgcn_readlane(nsl_l, l) + sj : __builtin_amdgcn_readlane(nsl_l, l) - 1 - sj;
+#else
       while (k < nw - 1 && g >= S.w[S.word[k]].seg0 + S.w[S.word[k]].nseg) k++;  // walks own consecutive segment ranges
       const int w = S.word[k];
-      if (w != cw) {  // the wave's segments of one walk are consecutive: flush once per walk
+      const int sg = g - S.w[w].seg0;
+#endif
+      if (w != cw) {  // walk-major: the wave's segments of one walk are consecutive, one flush per walk
         if (cw >= 0) flush_walk(S, cw, acc, accm, lane);
         cw = w; acc = 0.0; accm = 0.0;
       }
 #ifdef FSCLG_SEGSTATS
       if (lane == 0) atomicAdd(&S.cnt[6], 1ull);
 #endif
-      run_segment_idx<LDS, SEGN, SPLIT ? U_SPLIT : U_MAIN>(S, w, g - S.w[w].seg0, g - S.w[w].seg0 + 1, P, lane, acc,
-                                                           accm);
+      run_segment_idx<LDS, SEGN, SPLIT ? U_SPLIT : U_MAIN>(S, w, sg, sg + 1, P, lane, acc, accm);
       nsg_run++;
      }
     }
@@ -2251,10 +2310,10 @@ __device__ __forceinline__ void maxpos_body(SM& S, const Params& P) {
 #ifndef FSCLG_WPE_SPLIT
 #define FSCLG_WPE_SPLIT 6
 #endif
-template <bool LDS>
+template <bool LDS, bool BAND = false>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(FSCLG_WPE, FSCLG_WPE)))
 search_maxpos_kernel(Params P) {
-  __shared__ Smem S;
+  __shared__ SmemT<MAXWALK, BAND> S;
   maxpos_body<LDS, false>(S, P);
 }
 
@@ -3977,8 +4036,9 @@ static void plan_cache(fsclg_ctx* c) {
 #endif
 }
 
-// band mode by default where its window is narrow (K <= 6 intervals, C5); -1: the walk-window path
-static int band_default(const fsclg_ctx* c) { return c->c_civ_b > 0 && c->c_civ_b <= 6 ? 16 : -1; }
+// band mode is off by default (-1: the walk-window path with site-major dealing, faster at C4 and C5,
+// HISTORY §R6.2); FSCLG_BAND_TH=16 turns it on
+static int band_default(const fsclg_ctx* c) { (void)c; return -1; }
 
 static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int eval_range, int bp_resl) {
   const Slot& S = c->slot[slot];
@@ -3989,12 +4049,9 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   // dynamic LDS: the planned coefficient window, thresholds and null rows
   if (c->plan_dirty) plan_cache(c);
   {
-    // band mode where the LDS window is narrow (K <= 6 intervals: the coefficient planes of the
-    // large sample sizes, C5's n = 400 at K = 3), whose planes the vector L1 does not hold; with
-    // planes of a few KB (C2-C4) the walk-window path's global gathers hit L1 and band mode's
-    // layout costs more than it saves (HISTORY §R6.1).  FSCLG_BAND_TH overrides (-1: off); read per
-    // launch, as FSCLG_BAND_NB / FSCLG_BAND_MINP (tests switch them within one process).  Band
-    // mode's BandLds sits in the dynamic LDS after the logt copy, so its window is c_civ_b
+    // band mode (an alternative term order, off by default: HISTORY §R6.1-R6.2): FSCLG_BAND_TH >= 0
+    // turns it on; read per launch, as FSCLG_BAND_NB / FSCLG_BAND_MINP (tests switch them within one
+    // process).  Band mode's BandLds sits in the dynamic LDS after the logt copy, so its window is c_civ_b
     const int band_env = getenv("FSCLG_BAND_TH") ? atoi(getenv("FSCLG_BAND_TH")) : -2;
     const int band_th = band_env != -2 ? band_env : band_default(c);
     P.band_th = (c->d_dband && c->d_tpos && c->c_civ_b > 0) ? band_th : -1;
@@ -4088,11 +4145,14 @@ static int launch_blocks_impl(hipStream_t stream, const Params& P, int n) {
     if (dev >= 64 || !(attr_set >> dev & 1ull)) {
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat_m), "hipFuncSetAttribute");
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_kernel<true, true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat_m), "hipFuncSetAttribute");
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&search_maxpos_split_kernel<true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_WG - stat_s), "hipFuncSetAttribute");
       if (dev < 64) attr_set |= 1ull << dev;
     }
     if (P.split > 1) hipLaunchKernelGGL((search_maxpos_split_kernel<true>), dim3(grid), dim3(WG), dyn, stream, P);
+    else if (P.band_th >= 0 && P.n_civ > 0) hipLaunchKernelGGL((search_maxpos_kernel<true, true>), dim3(grid), dim3(WG), dyn, stream, P);
     else hipLaunchKernelGGL((search_maxpos_kernel<true>), dim3(grid), dim3(WG), dyn, stream, P);
   } else
     if (P.split > 1) hipLaunchKernelGGL((search_maxpos_split_kernel<false>), dim3(grid), dim3(WG), 0, stream, P);

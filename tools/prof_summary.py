@@ -47,8 +47,8 @@ if kt.exists():
     out["trace_union"] = {"calls": len(iv), "busy_ms": busy / 1e6,
                           "busy_ms_per_launch": busy / 1e6 / max(1, len(iv)),
                           "sum_ms": sum(e0 - s0 for s0, e0 in iv) / 1e6}
-pmc, pmc_ms = {}, {}
-for grp in ("fetch", "write", "sq", "f64"):
+pmc, pmc_ms, tot = {}, {}, defaultdict(float)
+for grp in ("fetch", "write", "sq", "f64", "mem", "tcc"):
     f = src / grp / "run_counter_collection.csv"
     if not f.exists():
         continue
@@ -56,6 +56,7 @@ for grp in ("fetch", "write", "sq", "f64"):
     for r in csv.DictReader(open(f)):
         if "search_maxpos" in r["Kernel_Name"]:
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
+            tot[r["Counter_Name"]] += float(r["Counter_Value"])
             n[r["Counter_Name"]] += 1
             dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     for k in agg:
@@ -69,6 +70,25 @@ if "FETCH_SIZE" in pmc:
     write = pmc.get("WRITE_SIZE", 0.0) * 1024
     out["hbm_bytes_per_launch"] = fetch + write
     out["hbm_bytes_note"] = "(FETCH_SIZE*2 + WRITE_SIZE) * 1024, MI355X_MICROARCH.md §HBM correction"
+# the memory path over the whole job (the mem / tcc passes): TA / TD busy cycles (summed over the CUs) and
+# L1 / L2 requests per SNP term, the L2 hit rate, and the HBM fetch bytes per term (the same job's terms)
+terms = None
+for name in ("bench_mem.json", "bench_tcc.json", "bench_fetch.json"):
+    p = src / name
+    if p.exists() and p.read_text().strip():
+        terms = json.loads(p.read_text().strip().splitlines()[-1])["stats"]["n_terms"]
+        break
+if terms and any(k in tot for k in ("TA_TA_BUSY_sum", "TCC_HIT_sum")):
+    mp = {"n_terms": terms, "per_term": {k: tot[k] / terms for k in ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum",
+                                                                      "TCP_TOTAL_CACHE_ACCESSES_sum",
+                                                                      "TCP_TCC_READ_REQ_sum") if k in tot}}
+    if "TCC_HIT_sum" in tot and "TCC_MISS_sum" in tot:
+        mp["tcc_hit_rate"] = tot["TCC_HIT_sum"] / max(1.0, tot["TCC_HIT_sum"] + tot["TCC_MISS_sum"])
+    if "FETCH_SIZE" in tot:
+        mp["hbm_fetch_bytes_per_term"] = tot["FETCH_SIZE"] * 1024 * 2 / terms
+    mp["note"] = ("counter totals over the job's search_maxpos dispatches / the job's SNP terms; TA/TD busy summed "
+                  "over the CUs (texture-path cycles per term on its CU)")
+    out["memory_path"] = mp
 for name in ("bench_trace.json", "bench_fetch.json"):
     p = src / name
     if p.exists() and p.read_text().strip():

@@ -1,5 +1,5 @@
 # rocprofv3 evidence for the bench's dominant kernel (run on the GPU box):
-#   [PASSES="trace fetch write sq f64"] bash tools/profile.sh <tag> [bench args...]
+#   [PASSES="trace fetch write sq f64 mem tcc"] bash tools/profile.sh <tag> [bench args...]
 # kernel-trace + stats in one pass, then one pass per PMC counter group (never combined with tracing);
 # PASSES selects a subset (a long job's passes can then go in separate calls, same output directory).
 set -e
@@ -9,13 +9,15 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 LIM=${PROF_LIMIT:-400}
-for p in ${PASSES:-trace fetch write sq f64}; do
+for p in ${PASSES:-trace fetch write sq f64 mem tcc}; do
   case $p in
     trace) args="--kernel-trace --stats" ;;
     fetch) args="--pmc FETCH_SIZE" ;;
     write) args="--pmc WRITE_SIZE" ;;
     sq)    args="--pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE" ;;
     f64)   args="--pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VMEM_WR SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 GRBM_GUI_ACTIVE" ;;
+    mem)   args="--pmc TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE GRBM_COUNT" ;;
+    tcc)   args="--pmc TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCP_PENDING_STALL_CYCLES_sum" ;;
     *) echo "unknown pass $p"; exit 2 ;;
   esac
   echo "[profile] $p $(date +%T)"
@@ -25,6 +27,6 @@ done
 # what a call may bring back; partial summaries of separate calls merge with tools/prof_merge.py
 if [ -n "$REDUCE" ]; then
   python3 $R/tools/prof_summary.py $OUT $OUT/partial_$(echo ${PASSES:-all} | tr ' ' '_') > /dev/null
-  for p in ${PASSES:-trace fetch write sq f64}; do rm -rf $OUT/$p; done
+  for p in ${PASSES:-trace fetch write sq f64 mem tcc}; do rm -rf $OUT/$p; done
 fi
 echo done
