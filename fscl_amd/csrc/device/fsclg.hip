@@ -6,7 +6,7 @@
 // for each point the alpha search of sm-search.c:269-300 as two phases (11 coarse, 14-15
 // refine candidates), two bisection levels per alpha search.  A phase evaluates every
 // candidate's bidirectional walk (sm-search.c:105-150) as a contiguous index range found by a
-// wave-parallel search (log(alpha*d) is monotone in |d|), cuts each walk part into 4096-site
+// wave-parallel search (log(alpha*d) is monotone in |d|), cuts each walk part into 2048-site
 // segments on the aligned 128-site trip grid, deals the segments round-robin to the 12 waves
 // (a trip: 128 sites, two per lane, one dwordx4 load of the interleaved site array), and sums
 // each walk EXACTLY as the reference's sequential `sm_logl += term` would, in any order:
@@ -68,7 +68,7 @@ namespace {
 constexpr int WG = FSCLG_WG;
 constexpr int NWAVE = WG / 64;
 #ifndef FSCLG_SEG
-#define FSCLG_SEG 4096
+#define FSCLG_SEG 2048
 #endif
 constexpr int SEG = FSCLG_SEG;     // terms per work segment
 #ifndef FSCLG_SEG_SPLIT
@@ -4037,7 +4037,7 @@ static void plan_cache(fsclg_ctx* c) {
 }
 
 // band mode is off by default (-1: the walk-window path with site-major dealing, faster at C4 and C5,
-// HISTORY §R6.2); FSCLG_BAND_TH=16 turns it on
+// HISTORY §R6.3); FSCLG_BAND_TH=16 turns it on
 static int band_default(const fsclg_ctx* c) { (void)c; return -1; }
 
 static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int eval_range, int bp_resl) {
@@ -4049,7 +4049,7 @@ static Params make_params(fsclg_ctx* c, Batch& B, int slot, int n, int mode, int
   // dynamic LDS: the planned coefficient window, thresholds and null rows
   if (c->plan_dirty) plan_cache(c);
   {
-    // band mode (an alternative term order, off by default: HISTORY §R6.1-R6.2): FSCLG_BAND_TH >= 0
+    // band mode (an alternative term order, off by default: HISTORY §R6.1, §R6.3): FSCLG_BAND_TH >= 0
     // turns it on; read per launch, as FSCLG_BAND_NB / FSCLG_BAND_MINP (tests switch them within one
     // process).  Band mode's BandLds sits in the dynamic LDS after the logt copy, so its window is c_civ_b
     const int band_env = getenv("FSCLG_BAND_TH") ? atoi(getenv("FSCLG_BAND_TH")) : -2;
