@@ -6,7 +6,11 @@ set -e
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$R/gpurun_out/prof_$TAG
-mkdir -p $OUT
+# PROF_TMP=1 (long jobs): the raw passes go to /tmp, and only the reduced summaries and the bench lines are
+# copied under gpurun_out/ -- a pass killed at the call's limit then leaves nothing large behind there
+FINAL=$OUT
+[ -n "$PROF_TMP" ] && OUT=/tmp/prof_$TAG
+mkdir -p $OUT $FINAL
 cd /tmp && export TMPDIR=/tmp
 LIM=${PROF_LIMIT:-400}
 for p in ${PASSES:-trace fetch write sq f64 mem tcc}; do
@@ -21,7 +25,7 @@ for p in ${PASSES:-trace fetch write sq f64 mem tcc}; do
     *) echo "unknown pass $p"; exit 2 ;;
   esac
   echo "[profile] $p $(date +%T)"
-  timeout -k 10 $LIM rocprofv3 $args --output-format csv -d $OUT/$p -o run -- python3 $R/bench.py "$@" > $OUT/bench_$p.json 2> $OUT/$p.err
+  timeout -k 10 $LIM rocprofv3 $args --output-format csv -d $OUT/$p -o run -- python3 $R/bench.py "$@" > $OUT/bench_$p.json 2> $FINAL/$p.err
 done
 # REDUCE=1: summarize on the box (tools/prof_summary.py) and drop the raw CSVs, which for a long job exceed
 # what a call may bring back; partial summaries of separate calls merge with tools/prof_merge.py
@@ -29,4 +33,5 @@ if [ -n "$REDUCE" ]; then
   python3 $R/tools/prof_summary.py $OUT $OUT/partial_$(echo ${PASSES:-all} | tr ' ' '_') > /dev/null
   for p in ${PASSES:-trace fetch write sq f64 mem tcc}; do rm -rf $OUT/$p; done
 fi
+[ "$OUT" != "$FINAL" ] && cp $OUT/partial_* $OUT/bench_*.json $FINAL/ 2>/dev/null
 echo done
