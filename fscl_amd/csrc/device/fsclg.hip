@@ -683,6 +683,9 @@ __device__ __forceinline__ double walk_sequential(const SM& S, const Walk& W, co
 // the j-th segment from the nearest site of every walk that reaches it, so the waves working at once
 // read the same sites and log-table entries for different alphas (logt(|d|) does not depend on alpha)
 // and those reads hit the vector L1.  0: the left grid from the walk's far end, walk-major dealing.
+#ifndef FSCLG_GROUP_TOL
+#define FSCLG_GROUP_TOL 2  // a window group takes the following walks whose window base is at most this far below
+#endif
 #ifndef FSCLG_SITE_MAJOR
 #define FSCLG_SITE_MAJOR 1
 #endif
@@ -1849,7 +1852,7 @@ __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
       const int l = __ffsll((unsigned long long)__ballot(act && rank == k)) - 1;
       const int wbk = __builtin_amdgcn_readlane(wb, l), lenk = __builtin_amdgcn_readlane(len, l),
                 s0k = __builtin_amdgcn_readlane(seg0, l);
-      if (lenk && (ng == 0 || wbk < gprev - 2)) {
+      if (lenk && (ng == 0 || wbk < gprev - FSCLG_GROUP_TOL)) {
         if (lane == 0) { S.gwb[ng] = wbk; S.gseg[ng] = s0k; S.gk[ng] = k; }
         ng++;
         gprev = wbk;
