@@ -683,6 +683,9 @@ __device__ __forceinline__ double walk_sequential(const SM& S, const Walk& W, co
 // the j-th segment from the nearest site of every walk that reaches it, so the waves working at once
 // read the same sites and log-table entries for different alphas (logt(|d|) does not depend on alpha)
 // and those reads hit the vector L1.  0: the left grid from the walk's far end, walk-major dealing.
+#ifndef FSCLG_FAR_FIRST
+#define FSCLG_FAR_FIRST 0  // site-major slices from the farthest inwards (1) or from the nearest SNP outwards (0)
+#endif
 #ifndef FSCLG_GROUP_TOL
 #define FSCLG_GROUP_TOL 2  // a window group takes the following walks whose window base is at most this far below
 #endif
@@ -1900,16 +1903,32 @@ __device__ __forceinline__ void eval_walks(SM& S, const Params& P) {
      const int k0 = __builtin_amdgcn_readfirstlane(S.gk[gi]), nwg = __builtin_amdgcn_readfirstlane(S.gk[gi + 1]) - k0;
      int wl = 0, nsl_l = 0, nsr_l = 0;
      if (lane < nwg) { wl = S.word[k0 + lane]; nsl_l = S.w[wl].nsl; nsr_l = S.w[wl].nseg - nsl_l; }
+#if FSCLG_FAR_FIRST
+     // the slices from the farthest inwards: the phase ends on the dense near slices (every walk
+     // reaches them), so the waves run out of work together
+     int jmax = max(nsl_l, nsr_l) - 1;
+#pragma unroll
+     for (int o = 32; o > 0; o >>= 1) jmax = max(jmax, __shfl_xor(jmax, o, 64));
+     jmax = __builtin_amdgcn_readfirstlane(jmax);
+     int base = __builtin_amdgcn_readfirstlane(S.gseg[gi]), sj = jmax, spart = 0;
+#else
      int base = __builtin_amdgcn_readfirstlane(S.gseg[gi]), sj = 0, spart = 0;
-     unsigned long long M = __ballot(lane < nwg && nsl_l > 0);
+#endif
+     unsigned long long M = __ballot(lane < nwg && (spart ? nsr_l : nsl_l) > sj);
      (void)k;
 #endif
      for (int g = __builtin_amdgcn_readfirstlane(S.gseg[gi]) + g0; g < ge; g += mstride) {
 #if FSCLG_SITE_MAJOR
+#if FSCLG_FAR_FIRST
+      while (g >= base + (int)__popcll(M) && sj >= 0) {  // g < ge: a later slice holds it
+        base += (int)__popcll(M);
+        if (spart == 0) spart = 1; else { spart = 0; sj--; }
+#else
       while (g >= base + (int)__popcll(M) && sj < MAXSEG_W) {  // g < ge: a later slice holds it
         base += (int)__popcll(M);
         if (spart == 0) spart = 1; else { spart = 0; sj++; }
-        M = __ballot(lane < nwg && (spart ? nsr_l : nsl_l) > sj);
+#endif
+        M = __ballot(lane < nwg && (!FSCLG_FAR_FIRST || sj >= 0) && (spart ? nsr_l : nsl_l) > sj);
       }
       if (g >= base + (int)__popcll(M)) break;  // never: the slices hold exactly the group's segments
       const int rk = g - base;  // the rk-th walk of the slice
